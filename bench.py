@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X batched key hasher (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N ... bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Workload (BASELINE.json configs[1]): fnv1a_64 over 2^26 keys
+per GPU with Zipf lengths 8-64 B (s = 1.0), synthetic bytes 0x00-0xFF,
+device-resident. A step = one kernel pass over one rank's batch. For N > 1
+rank 0 generates all N x 2^26 keys and scatters byte-balanced ranges over
+RCCL (grouped point-to-point); scatter time is reported separately and is
+not part of `value` (weak scaling: fixed keys per GPU).
+
+Rank 0 prints ONE JSON line. `value` = total keys hashed by all ranks per
+second (Mkeys/s) over K timed steps, max over ranks. Extra fields: the md5
+rate on the same keys, the C3 shape (2^26 x 32 B, fnv1a_64) the north-star
+70 % roofline target is quoted on, the HBM roofline of the dominant kernel
+(HIP events on the launch stream), and the reference CPU hashkit timed on
+this host (rank 0, N = 1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
+METRIC = "Mkeys/s + GB/s hashed (device-resident), fnv1a_64 & md5, 1/2/4/8 MI355X"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--nkeys", type=int, default=1 << 26, help="keys per GPU")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--no-extra", action="store_true", help="skip md5 / C3 secondary measurements")
+    p.add_argument("--cpu-sample", type=int, default=1 << 24, help="keys in the CPU baseline sample")
+    return p.parse_args()
+
+
+def timed_steps(t, torch, mode, keys, off, out, steps, warmup, dist_on):
+    """W untimed + K timed launches; wall time bracketed by barrier+sync,
+    kernel time by HIP events recorded on the launch stream."""
+    for _ in range(warmup):
+        t.hash_batch_device(mode, keys, off, out)
+    torch.cuda.synchronize()
+    if dist_on:
+        import torch.distributed as dist
+
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        t.hash_batch_device(mode, keys, off, out, stream=stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / steps
+    return wall, kern_ms
+
+
+def max_over_ranks(torch, x: float, dist_on: bool) -> float:
+    if not dist_on:
+        return x
+    import torch.distributed as dist
+
+    v = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    return float(v.item())
+
+
+def sum_over_ranks(torch, x: float, dist_on: bool) -> float:
+    if not dist_on:
+        return x
+    import torch.distributed as dist
+
+    v = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(v, op=dist.ReduceOp.SUM)
+    return float(v.item())
+
+
+def roofline(alg_bytes: float, kern_ms: float, traffic):
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+
+
+def load_traffic(kernel_mode: str, workload: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
+    workload (profiles/pmc_*.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950
+    correction), or None when no such measurement exists."""
+    import glob
+
+    best = None
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_*.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        rec = d.get("workloads", {}).get(workload, {}).get(kernel_mode)
+        if rec and "hbm_bytes_per_launch" in rec:
+            best = {"bytes_per_launch": rec["hbm_bytes_per_launch"], "source": os.path.relpath(path, HERE)}
+    return best
+
+
+def cpu_baseline(t, spec, n, mode_names, reps=3):
+    """Reference hashkit (oracle/_ref, compiled from /root/reference) or, when
+    that build is absent, the repo's C restatement, timed on this host."""
+    from tests.oracle_lib import Oracle, RefHashkit
+
+    if RefHashkit.available():
+        impl, kind = RefHashkit(), "reference"
+    else:
+        impl, kind = Oracle(), "port"
+    keys, off = t.synth_host(spec, 0, n)
+    nbytes = int(off[-1])
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    res = {}
+    for name in mode_names:
+        m = t.HASH_NAMES.index(name)
+        s1 = impl.time_batch(m, keys, off, 1, reps)
+        sN = impl.time_batch(m, keys, off, threads, reps)
+        res[name] = {"mkeys_s_1thread": round(n / s1 / 1e6, 2), "gbs_1thread": round(nbytes / s1 / 1e9, 3),
+                     f"mkeys_s_{threads}threads": round(n / sN / 1e6, 2),
+                     f"gbs_{threads}threads": round(nbytes / sN / 1e9, 3)}
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    head = res[mode_names[0]]
+    return {"value": head[f"mkeys_s_{threads}threads"], "unit": "Mkeys/s", "cores": threads, "kind": kind,
+            "sample": f"first {n} keys of the same workload ({nbytes} key bytes), {mode_names[0]}, "
+                      f"best of {reps} after a warm-up, per-key hash_t calls on {threads} pthreads over "
+                      f"byte-balanced ranges; single-thread and md5 alongside",
+            "cpu_model": cpu_model, "detail": res}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    torch.cuda.set_device(local)
+    dist_on = world > 1
+    if dist_on:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import twemproxy_amd as t
+    from twemproxy_amd.shard import scatter_shards
+
+    spec = t.CONFIGS["C2"]["spec"]
+    n_local = args.nkeys
+    dev = torch.device("cuda", local)
+
+    # ---- input: device-resident before the timed region
+    scatter = None
+    if dist_on:
+        import torch.distributed as dist
+
+        full_k = full_o = None
+        if rank == 0:
+            full_k, full_o = t.synth_device(spec, 0, n_local * world, device=dev)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        keys, off, first = scatter_shards(full_k, full_o, dev)
+        torch.cuda.synchronize()
+        dist.barrier()
+        sc_s = time.perf_counter() - t0
+        moved = int(full_k.numel() + full_o.numel() * 8) if rank == 0 else 0
+        del full_k, full_o
+        torch.cuda.empty_cache()
+        scatter = {"ms": round(sc_s * 1e3, 2), "root_egress_bytes": moved}
+    else:
+        keys, off = t.synth_device(spec, 0, n_local, device=dev)
+        first = 0
+    nk = off.numel() - 1
+    key_bytes = int(off[-1].item())
+    out = torch.empty(nk, dtype=torch.int32, device=dev)
+
+    # ---- headline: fnv1a_64
+    wall, kern_ms = timed_steps(t, torch, "fnv1a_64", keys, off, out, args.steps, args.warmup, dist_on)
+    wall = max_over_ranks(torch, wall, dist_on)
+    kern_ms_max = max_over_ranks(torch, kern_ms, dist_on)
+    total_keys = sum_over_ranks(torch, float(nk), dist_on) * args.steps
+    total_bytes = sum_over_ranks(torch, float(key_bytes), dist_on) * args.steps
+    value = total_keys / wall / 1e6
+    alg = key_bytes + 12.0 * nk  # key bytes + u64 offset + u32 hash per key
+    rf = roofline(alg, kern_ms, load_traffic("fnv1a_64", "C2"))
+
+    res = {
+        "metric": METRIC, "value": round(value, 1), "unit": "Mkeys/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64 counter generator, SURVEY.md §8d seed 2)",
+        "config": {"workload": f"C2: fnv1a_64 over {n_local} keys per GPU, Zipf lengths 8-64 B (s=1.0, "
+                               "mean ~19.3 B), bytes 0x00-0xFF, device-resident",
+                   "hash": "fnv1a_64", "nkeys_per_gpu": n_local, "key_bytes_rank0": key_bytes,
+                   "parallelism": f"shard{world}" if world > 1 else "single"},
+        "gb_per_s_hashed": round(total_bytes / wall / 1e9, 2),
+        "kernel_ms_rank0": round(kern_ms, 4), "kernel_ms_max": round(kern_ms_max, 4),
+        "roofline": rf,
+    }
+    if scatter:
+        res["scatter"] = scatter
+
+    # ---- md5 on the same keys; C3 shape for the 70 % target
+    if not args.no_extra:
+        w5, k5 = timed_steps(t, torch, "md5", keys, off, out, max(3, args.steps // 4), 1, dist_on)
+        w5 = max_over_ranks(torch, w5, dist_on)
+        s5 = max(3, args.steps // 4)
+        res["md5"] = {"value": round(sum_over_ranks(torch, float(nk), dist_on) * s5 / w5 / 1e6, 1),
+                      "unit": "Mkeys/s", "gb_per_s_hashed": round(sum_over_ranks(torch, float(key_bytes), dist_on) * s5 / w5 / 1e9, 2),
+                      "roofline": roofline(alg, k5, load_traffic("md5", "C2"))}
+        del keys, off, out
+        torch.cuda.empty_cache()
+        c3 = t.CONFIGS["C3"]["spec"]
+        keys3, off3 = t.synth_device(c3, first, n_local, device=dev)
+        out3 = torch.empty(n_local, dtype=torch.int32, device=dev)
+        w3, k3 = timed_steps(t, torch, "fnv1a_64", keys3, off3, out3, args.steps, args.warmup, dist_on)
+        w3 = max_over_ranks(torch, w3, dist_on)
+        kb3 = int(off3[-1].item())
+        res["c3_fnv1a_64"] = {
+            "workload": f"C3 shape: fnv1a_64 over {n_local} x 32 B keys per GPU",
+            "value": round(sum_over_ranks(torch, float(n_local), dist_on) * args.steps / w3 / 1e6, 1),
+            "unit": "Mkeys/s", "kernel_ms": round(k3, 4),
+            "roofline": roofline(kb3 + 12.0 * n_local, k3, load_traffic("fnv1a_64", "C3"))}
+        del keys3, off3, out3
+
+    # ---- CPU baseline (rank 0, N = 1)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            res["cpu_baseline"] = cpu_baseline(t, spec, args.cpu_sample, ["fnv1a_64", "md5"])
+        except Exception as e:  # reported, never substituted for the GPU number
+            res["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist_on:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+/*
+ * nc_gpuhash — MI355X (gfx950) batched key hashing, a drop-in for twemproxy's
+ * src/hashkit.
+ *
+ * C ABI only: plain pointers and sizes, no C++ or torch types. Link
+ * libnc_gpuhash.so in place of libhashkit.a (src/hashkit/Makefile.am:8-23,
+ * src/Makefile.am:58). Reference interfaces each entry point replaces are cited
+ * as /root/reference/<path>:<line>.
+ *
+ * Four groups:
+ *   1. Link-compatible per-key symbols with the exact prototypes of
+ *      src/hashkit/nc_hashkit.h:57-69 (+ ketama_hash, src/hashkit/nc_ketama.c:31).
+ *      These are host functions: a per-key GPU round trip costs more than the
+ *      hash. The batched entry points below never call them.
+ *   2. The hash: selector (src/nc_conf.c:1738-1764, hash_algos[] :30-35).
+ *   3. Batched GPU hashing over an offset CSR: key i is
+ *      keys[offsets[i] .. offsets[i+1]). Device-resident, synchronous host and
+ *      asynchronous (ticket + poll) host forms. There is no CPU fallback: with
+ *      no usable GPU they return NC_ERROR with errno ENODEV.
+ *   4. Multi-GPU shard planning (byte-balanced key ranges).
+ */
+#ifndef NC_GPUHASH_H
+#define NC_GPUHASH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* rstatus_t and its values, src/nc_core.h:61-69. Guarded so the header can be
+ * included next to nc_core.h inside twemproxy. */
+#ifndef _NC_CORE_H_
+typedef int rstatus_t;
+#define NC_OK     0
+#define NC_ERROR -1
+#define NC_EAGAIN -2
+#define NC_ENOMEM -3
+#endif
+
+/* Mode ids are hash_type_t values in HASH_CODEC order
+ * (src/hashkit/nc_hashkit.h:24-48). */
+typedef enum nc_gpuhash_mode {
+    NC_GPUHASH_ONE_AT_A_TIME = 0,
+    NC_GPUHASH_MD5 = 1,
+    NC_GPUHASH_CRC16 = 2,
+    NC_GPUHASH_CRC32 = 3,
+    NC_GPUHASH_CRC32A = 4,
+    NC_GPUHASH_FNV1_64 = 5,
+    NC_GPUHASH_FNV1A_64 = 6,   /* conf default, src/nc_conf.h:44 */
+    NC_GPUHASH_FNV1_32 = 7,
+    NC_GPUHASH_FNV1A_32 = 8,
+    NC_GPUHASH_HSIEH = 9,
+    NC_GPUHASH_MURMUR = 10,
+    NC_GPUHASH_JENKINS = 11,
+    NC_GPUHASH_NMODES = 12     /* HASH_SENTINEL */
+} nc_gpuhash_mode_t;
+
+/* Bytes that must stay readable after offsets[nkeys] in a device key buffer
+ * handed to nc_gpuhash_batch_device (16-byte vector loads of the last key). */
+#define NC_GPUHASH_PAD 32
+
+/* ---- 1. per-key, link-compatible (src/hashkit/nc_hashkit.h:57-69) ---- */
+uint32_t hash_one_at_a_time(const char *key, size_t key_length);
+void md5_signature(const unsigned char *key, unsigned int length, unsigned char *result);
+uint32_t hash_md5(const char *key, size_t key_length);
+uint32_t hash_crc16(const char *key, size_t key_length);
+uint32_t hash_crc32(const char *key, size_t key_length);
+uint32_t hash_crc32a(const char *key, size_t key_length);
+uint32_t hash_fnv1_64(const char *key, size_t key_length);
+uint32_t hash_fnv1a_64(const char *key, size_t key_length);
+uint32_t hash_fnv1_32(const char *key, size_t key_length);
+uint32_t hash_fnv1a_32(const char *key, size_t key_length);
+uint32_t hash_hsieh(const char *key, size_t key_length);
+uint32_t hash_jenkins(const char *key, size_t length);
+uint32_t hash_murmur(const char *key, size_t length);
+/* src/hashkit/nc_ketama.c:31-41 */
+uint32_t ketama_hash(const char *key, size_t key_length, uint32_t alignment);
+
+/* ---- 2. hash: selector (src/nc_conf.c:1738-1764) ---- */
+/* Name -> mode id; -1 with errno EINVAL for "is not a valid hash". */
+int nc_gpuhash_mode_from_name(const char *name, size_t len);
+/* Mode id -> HASH_CODEC name ("fnv1a_64", ...); NULL for an invalid id. */
+const char *nc_gpuhash_mode_name(int mode);
+
+/* ---- 3a. device-resident batch ----
+ * d_keys, d_offsets (nkeys + 1 entries, non-decreasing) and d_out (nkeys)
+ * are device pointers; d_keys must stay readable NC_GPUHASH_PAD bytes past
+ * offsets[nkeys]. Enqueues on `stream` (a hipStream_t, NULL = default
+ * stream) and returns without waiting. Output order is input key order
+ * (frag_seq[] depends on it, src/proto/nc_memcache.c:1337). */
+rstatus_t nc_gpuhash_batch_device(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
+                                  uint64_t nkeys, uint32_t *d_out, void *stream);
+
+/* Same launch repeated `iters` times between two hipEvents recorded on
+ * `stream`; blocks until done and stores the mean milliseconds per launch. */
+rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
+                                 uint64_t nkeys, uint32_t *d_out, void *stream,
+                                 int iters, float *avg_ms);
+
+/* Launch tuning (process-wide; for tests and benchmarks). grid_cap: maximum
+ * workgroups per launch (0 = one per 256-key tile, -1 = keep). sort: group a
+ * tile's keys by length class before hashing (1 on, 0 off, -1 keep). */
+rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort);
+
+/* ---- 3b. host batches through a context (pinned staging, one stream per slot) ---- */
+typedef struct nc_gpuhash_ctx nc_gpuhash_ctx_t;
+
+/* A borrowed key span inside an mbuf, the shape of struct keypos
+ * (src/nc_message.h:232-235). */
+struct nc_keyspan {
+    const uint8_t *start;
+    const uint8_t *end;
+};
+
+/* Create a context on `device` able to take batches of up to max_keys keys
+ * and max_key_bytes key bytes, with `nslots` in-flight batches (>= 1). */
+nc_gpuhash_ctx_t *nc_gpuhash_ctx_create(int device, uint64_t max_keys, uint64_t max_key_bytes,
+                                        int nslots);
+void nc_gpuhash_ctx_destroy(nc_gpuhash_ctx_t *ctx);
+
+/* Pack a CSR batch into a free slot's pinned staging, enqueue H2D, kernel and
+ * D2H, and return a ticket without blocking. NC_EAGAIN if every slot is busy,
+ * NC_ENOMEM if the batch exceeds the context's limits. The caller may reuse
+ * keys/offsets as soon as this returns (they are copied, as mbufs are
+ * recycled after msg_put, src/nc_mbuf.c:118-128). */
+rstatus_t nc_gpuhash_submit(nc_gpuhash_ctx_t *ctx, int mode, const uint8_t *keys,
+                            const uint64_t *offsets, uint32_t nkeys, uint32_t *out, int *ticket);
+/* The same from keypos-style spans (the fragment loops,
+ * src/proto/nc_memcache.c:1324-1345, src/proto/nc_redis.c:2862-2901). */
+rstatus_t nc_gpuhash_submit_spans(nc_gpuhash_ctx_t *ctx, int mode, const struct nc_keyspan *spans,
+                                  uint32_t nkeys, uint32_t *out, int *ticket);
+/* NC_OK once the ticket's hashes are in its `out`, NC_EAGAIN while pending. */
+rstatus_t nc_gpuhash_poll(nc_gpuhash_ctx_t *ctx, int ticket);
+/* Block until the ticket completes. */
+rstatus_t nc_gpuhash_wait(nc_gpuhash_ctx_t *ctx, int ticket);
+
+/* One synchronous host batch on a process-wide context (device 0), the
+ * SURVEY.md §8b.2 shape. */
+rstatus_t nc_hashkit_batch(int mode, const uint8_t *keys, const uint64_t *offsets,
+                           uint32_t nkeys, uint32_t *out);
+
+/* ---- 4. multi-GPU shard planning ----
+ * Split keys [0, nkeys) into nshards contiguous ranges with about equal key
+ * bytes: key_bounds[g] .. key_bounds[g+1] is shard g (nshards + 1 entries). */
+rstatus_t nc_gpuhash_shard_bounds(const uint64_t *offsets, uint64_t nkeys, uint32_t nshards,
+                                  uint64_t *key_bounds);
+
+/* ---- info ---- */
+/* Number of visible GPUs (0 when none); never initialises more than HIP's
+ * device query does. */
+int nc_gpuhash_device_count(void);
+/* Library version string. */
+const char *nc_gpuhash_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NC_GPUHASH_H */

@@ -1,0 +1,130 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+symbol include/*.h declares, and its host logic (selector, per-key link-compat
+symbols, shard planning, synthetic generator) behaves like the reference."""
+import ctypes
+import errno
+import os
+import re
+
+import numpy as np
+import pytest
+
+import twemproxy_amd as t
+from twemproxy_amd import _lib as L
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def declared_functions():
+    names = set()
+    for h in ("nc_gpuhash.h", "nc_gpuhash_synth.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\(", src, flags=re.M):
+            if m.group(1) not in ("defined",):
+                names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(L.LIB_PATH)
+    names = declared_functions()
+    assert len(names) >= 34
+    missing = [n for n in sorted(names) if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the ctypes binding covers exactly the declared surface
+    assert names == set(L.SIGNATURES), names ^ set(L.SIGNATURES)
+
+
+def test_library_has_gfx950_code_object():
+    blob = open(L.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+    assert b"nc_hash_kernel" in blob
+
+
+def test_selector_matches_conf_set_hash():
+    for m, name in enumerate(t.HASH_NAMES):
+        assert t.conf_set_hash(name) == m
+        assert L.lib().nc_gpuhash_mode_name(m).decode() == name
+    assert t.conf_set_hash(t.HASH_DEFAULT) == 6
+    for bad in ("", "fnv1a", "FNV1A_64", "fnv1a_64 ", "md5\0"):
+        with pytest.raises(ValueError, match="is not a valid hash"):
+            t.conf_set_hash(bad)
+    assert L.lib().nc_gpuhash_mode_name(12) is None
+    assert L.lib().nc_gpuhash_mode_name(-1) is None
+
+
+def test_per_key_symbols_match_golden_corpus(corpus):
+    keys, offsets, expected = corpus
+    raw = keys.tobytes()
+    for m, name in enumerate(t.HASH_NAMES):
+        fn = getattr(L.lib(), "hash_" + name)
+        got = [fn(raw[offsets[i]:offsets[i + 1]], int(offsets[i + 1] - offsets[i])) for i in range(offsets.size - 1)]
+        np.testing.assert_array_equal(np.array(got, dtype=np.uint32), expected[m], err_msg=name)
+
+
+def test_per_key_symbols_kats(kat):
+    for name, want in kat["apple"].items():
+        assert t.hash_key(name, b"apple") == want
+    assert t.ketama_hash(b"server1-8", 0) == kat["ketama_server1-8"]["0"]
+    assert t.ketama_hash(b"server1-8", 3) == kat["ketama_server1-8"]["3"]
+    import hashlib
+
+    for k in (b"", b"a", b"x" * 55, b"y" * 56, b"z" * 64, b"q" * 200):
+        assert t.md5_signature(k) == hashlib.md5(k).digest()
+
+
+def test_shard_bounds_byte_balanced():
+    rng = np.random.default_rng(0)
+    lens = rng.integers(0, 300, size=10001).astype(np.uint64)
+    off = np.zeros(lens.size + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    for g in (1, 2, 3, 4, 7, 8):
+        b = t.shard_bounds(off, g)
+        assert b[0] == 0 and b[-1] == lens.size and np.all(np.diff(b.astype(np.int64)) >= 0)
+        shard_bytes = off[b[1:]] - off[b[:-1]]
+        assert shard_bytes.max() - shard_bytes.min() <= 2 * 300
+        # each cut is the lower bound of its byte quantile
+        for i in range(1, g):
+            target = off[-1] * i // g
+            assert off[b[i]] >= target and (b[i] == 0 or off[b[i] - 1] < target)
+
+
+def test_shard_bounds_degenerate():
+    off = np.zeros(11, dtype=np.uint64)  # ten empty keys
+    np.testing.assert_array_equal(t.shard_bounds(off, 4), [0, 2, 5, 7, 10])
+    off = np.array([0], dtype=np.uint64)  # no keys
+    np.testing.assert_array_equal(t.shard_bounds(off, 3), [0, 0, 0, 0])
+
+
+def test_synth_host_is_shard_invariant():
+    spec = t.SynthSpec.zipf(2)
+    kb, ob = t.synth_host(spec, 0, 5000)
+    k2, o2 = t.synth_host(spec, 1234, 1000)
+    np.testing.assert_array_equal(np.diff(o2), np.diff(ob)[1234:2234])
+    np.testing.assert_array_equal(k2[: int(o2[-1])], kb[int(ob[1234]): int(ob[2234])])
+    lens = np.diff(ob)
+    assert lens.min() >= 8 and lens.max() <= 64
+    assert 17.0 < lens.mean() < 22.0  # mean ~19.3 B
+    kp, op = t.synth_host(t.SynthSpec.fixed(5, 40, t.BYTES_PRINTABLE), 0, 100)
+    body = kp[: int(op[-1])]
+    assert body.min() >= 0x21 and body.max() <= 0x7E
+
+
+def test_synth_rejects_bad_spec():
+    with pytest.raises(t.NcError):
+        t.synth_host(t.SynthSpec(1, 1, 8, 200), 0, 10)  # zipf range > 64
+    with pytest.raises(t.NcError):
+        t.synth_host(t.SynthSpec(1, 7, 8, 8), 0, 10)  # unknown distribution
+
+
+@pytest.mark.skipif(t.device_count() > 0, reason="checks the no-GPU failure mode")
+def test_batched_path_fails_loudly_without_gpu():
+    keys, off = t.pack_keys([b"apple"])
+    with pytest.raises(t.NcError) as ei:
+        t.hash_batch_host("fnv1a_64", keys, off)
+    assert ei.value.errno == errno.ENODEV
+    with pytest.raises(t.NcError):
+        t.Context()
+    rc = L.lib().nc_gpuhash_batch_device(99, None, None, 1, None, None)
+    assert rc == L.NC_ERROR and ctypes.get_errno() == errno.EINVAL

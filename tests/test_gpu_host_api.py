@@ -1,0 +1,84 @@
+"""Host-side batch API on the GPU: synchronous nc_hashkit_batch, the
+asynchronous context (submit / poll / wait), keypos-style spans, and the
+error returns of SURVEY.md §8b.3."""
+import numpy as np
+import pytest
+
+import twemproxy_amd as t
+
+pytestmark = pytest.mark.gpu
+
+
+def test_hashkit_batch_sync(gpu, corpus):
+    keys, off, expected = corpus
+    for m in range(12):
+        np.testing.assert_array_equal(t.hash_batch_host(m, keys, off), expected[m])
+    assert t.hash_keys("fnv1a_64", [b"apple"]) == [1488911807]
+
+
+def test_hashkit_batch_grows_context(gpu, oracle):
+    keys, off = t.synth_host(t.SynthSpec.zipf(9), 0, 300000)
+    np.testing.assert_array_equal(t.hash_batch_host("murmur", keys, off), oracle.batch(10, keys, off))
+
+
+def test_context_async_slots(gpu, oracle):
+    with t.Context(max_keys=4096, max_key_bytes=1 << 20, nslots=2) as ctx:
+        batches = [t.synth_host(t.SynthSpec.zipf(20 + i), 0, 3000) for i in range(6)]
+        tickets = []
+        for i, (k, o) in enumerate(batches[:2]):
+            tickets.append(ctx.submit("fnv1a_64", k, o))
+        # a third submit while both slots are in flight returns NC_EAGAIN, unless
+        # a slot already completed (then it is recycled and its output delivered)
+        try:
+            tickets.append(ctx.submit("fnv1a_64", *batches[2]))
+            third = True
+        except BlockingIOError:
+            third = False
+        for tk, out in tickets:
+            ctx.wait(tk)
+        for (k, o), (_, out) in zip(batches[: len(tickets)], tickets):
+            np.testing.assert_array_equal(out, oracle.batch(6, k, o))
+        # poll loop over the rest, the way core_loop would
+        pending = []
+        for k, o in batches[(3 if third else 2):]:
+            while True:
+                try:
+                    pending.append((ctx.submit("md5", k, o), k, o))
+                    break
+                except BlockingIOError:
+                    for (tk, _), _, _ in pending:
+                        ctx.poll(tk)
+        for (tk, out), k, o in pending:
+            while not ctx.poll(tk):
+                pass
+            np.testing.assert_array_equal(out, oracle.batch(1, k, o))
+
+
+def test_context_spans_from_mbuf(gpu, oracle):
+    """Keys borrowed from a 16 KiB mbuf-like buffer as (start, end) spans."""
+    rng = np.random.default_rng(5)
+    mbuf = rng.integers(0x21, 0x7F, size=16336, dtype=np.uint8)
+    spans, pos = [], 0
+    while True:
+        n = int(rng.integers(1, 64))
+        if pos + n + 2 > mbuf.size:
+            break
+        spans.append((pos, pos + n))
+        pos += n + 2  # "\r\n"-like separator between keys
+    with t.Context(max_keys=2048, max_key_bytes=1 << 16) as ctx:
+        tk, out = ctx.submit_spans("fnv1a_64", mbuf, spans)
+        ctx.wait(tk)
+    want = [oracle.hash(6, mbuf[s:e].tobytes()) for s, e in spans]
+    assert out.tolist() == want
+
+
+def test_context_limits(gpu):
+    with t.Context(max_keys=16, max_key_bytes=64) as ctx:
+        k, o = t.pack_keys([b"x" * 10] * 17)
+        with pytest.raises(t.NcError):  # NC_ENOMEM: too many keys
+            ctx.submit("md5", k, o)
+        k, o = t.pack_keys([b"x" * 65])
+        with pytest.raises(t.NcError):  # NC_ENOMEM: too many bytes
+            ctx.submit("md5", k, o)
+        with pytest.raises(ValueError):
+            ctx.submit("sha1", k, o)

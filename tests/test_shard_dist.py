@@ -1,0 +1,78 @@
+"""Multi-rank sharding on CPU (gloo, world_size 2 and 3): byte-balanced bounds,
+the root scatter, and that the shards' hashes reassemble to the full batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import twemproxy_amd as t
+from twemproxy_amd.shard import plan_bounds, scatter_shards
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, spec_args, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.oracle_lib import Oracle
+
+        spec = t.SynthSpec(*spec_args)
+        keys_np, off_np = t.synth_host(spec, 0, n)
+        keys = torch.from_numpy(keys_np) if rank == 0 else None
+        off = torch.from_numpy(off_np.astype(np.int64)) if rank == 0 else None
+        lk, lo, first = scatter_shards(keys, off, torch.device("cpu"))
+        lo_np = lo.numpy().astype(np.uint64)
+        oracle = Oracle()
+        mine = oracle.batch(6, lk.numpy(), lo_np, threads=1)
+        full = oracle.batch(6, keys_np, off_np, threads=1)
+        ok = np.array_equal(mine, full[first: first + lo_np.size - 1])
+        # pad after the shard's last key is zero and present
+        ok &= lk.numel() == int(lo_np[-1]) + t.NC_GPUHASH_PAD
+        q.put((rank, bool(ok), first, lo_np.size - 1, int(lo_np[-1])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("spec_args,n", [((2, t.hashkit.SYNTH_ZIPF, 8, 57), 20000),
+                                         ((6, t.hashkit.SYNTH_UNIFORM, 0, 600), 3000)])
+def test_scatter_and_hash_shards(world, spec_args, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, spec_args, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] for r in res), res
+    # contiguous cover of [0, n), byte-balanced
+    starts = [r[2] for r in res]
+    counts = [r[3] for r in res]
+    assert starts[0] == 0 and sum(counts) == n
+    assert all(starts[i] + counts[i] == starts[i + 1] for i in range(world - 1))
+    bytes_ = [r[4] for r in res]
+    assert max(bytes_) - min(bytes_) <= 2 * 600
+
+
+def test_plan_bounds_matches_c_shard_bounds():
+    for spec in (t.SynthSpec.zipf(2), t.SynthSpec.uniform(6, 0, 600), t.SynthSpec.fixed(3, 32)):
+        _, off = t.synth_host(spec, 0, 12345)
+        for g in (1, 2, 3, 4, 5, 8):
+            want = t.shard_bounds(off, g).astype(np.int64)
+            got = plan_bounds(torch.from_numpy(off.astype(np.int64)), g).numpy()
+            np.testing.assert_array_equal(got, want)
+    off = np.zeros(9, dtype=np.int64)
+    np.testing.assert_array_equal(plan_bounds(torch.from_numpy(off), 4).numpy(),
+                                  t.shard_bounds(off.astype(np.uint64), 4).astype(np.int64))

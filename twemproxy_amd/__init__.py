@@ -1,0 +1,41 @@
+"""twemproxy_amd — MI355X-native batched key hashing, a drop-in for twemproxy's src/hashkit.
+
+The product is the C-ABI library ``libnc_gpuhash.so`` (include/nc_gpuhash.h):
+hand-written gfx950 HIP kernels for the 12 hashkit modes behind a C host layer.
+This package is the Python mirror of the reference interface used by the
+tests and the benchmark.
+"""
+from ._lib import LIB_PATH, NC_EAGAIN, NC_ENOMEM, NC_ERROR, NC_GPUHASH_PAD, NC_OK, NcError, lib
+from .hashkit import (
+    BYTES_FULL,
+    BYTES_PRINTABLE,
+    CONFIGS,
+    DIST_NAMES,
+    HASH_DEFAULT,
+    HASH_NAMES,
+    NMODES,
+    Context,
+    SynthSpec,
+    conf_set_hash,
+    device_count,
+    hash_batch_device,
+    hash_batch_host,
+    hash_key,
+    hash_keys,
+    ketama_hash,
+    md5_signature,
+    mode_of,
+    pack_keys,
+    shard_bounds,
+    synth_device,
+    synth_host,
+    time_batch_device,
+)
+
+__all__ = [
+    "LIB_PATH", "NC_EAGAIN", "NC_ENOMEM", "NC_ERROR", "NC_GPUHASH_PAD", "NC_OK", "NcError", "lib",
+    "BYTES_FULL", "BYTES_PRINTABLE", "CONFIGS", "DIST_NAMES", "HASH_DEFAULT", "HASH_NAMES", "NMODES",
+    "Context", "SynthSpec", "conf_set_hash", "device_count", "hash_batch_device", "hash_batch_host",
+    "hash_key", "hash_keys", "ketama_hash", "md5_signature", "mode_of", "pack_keys", "shard_bounds",
+    "synth_device", "synth_host", "time_batch_device",
+]

@@ -1,0 +1,147 @@
+"""ctypes binding of libnc_gpuhash.so (include/nc_gpuhash.h, include/nc_gpuhash_synth.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or ``make -C
+twemproxy_amd/csrc``). Loading fails loudly when it is missing: there is no
+Python or CPU fallback for the batched path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnc_gpuhash.so")
+
+NC_OK, NC_ERROR, NC_EAGAIN, NC_ENOMEM = 0, -1, -2, -3
+NC_GPUHASH_PAD = 32
+
+_lock = threading.Lock()
+_lib = None
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+class NcSynthSpec(ctypes.Structure):
+    """struct nc_synth_spec (include/nc_gpuhash_synth.h)."""
+
+    _fields_ = [
+        ("seed", ctypes.c_uint64),
+        ("len_dist", ctypes.c_int32),
+        ("len_a", ctypes.c_uint32),
+        ("len_b", ctypes.c_uint32),
+        ("charset", ctypes.c_int32),
+        ("zipf_s", ctypes.c_double),
+    ]
+
+
+class NcKeySpan(ctypes.Structure):
+    """struct nc_keyspan — the shape of twemproxy's struct keypos (src/nc_message.h:232-235)."""
+
+    _fields_ = [("start", ctypes.c_void_p), ("end", ctypes.c_void_p)]
+
+
+# name -> (restype, argtypes); every symbol include/*.h declares.
+SIGNATURES = {
+    # per-key, src/hashkit/nc_hashkit.h:57-69
+    "hash_one_at_a_time": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "md5_signature": (None, [ctypes.c_char_p, ctypes.c_uint, ctypes.c_char_p]),
+    "hash_md5": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "hash_crc16": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "hash_crc32": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "hash_crc32a": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "hash_fnv1_64": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "hash_fnv1a_64": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "hash_fnv1_32": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "hash_fnv1a_32": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "hash_hsieh": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "hash_jenkins": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "hash_murmur": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t]),
+    "ketama_hash": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]),
+    # selector
+    "nc_gpuhash_mode_from_name": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "nc_gpuhash_mode_name": (ctypes.c_char_p, [ctypes.c_int]),
+    # batches
+    "nc_gpuhash_batch_device": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p],
+    ),
+    "nc_gpuhash_time_device": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_int, ctypes.POINTER(ctypes.c_float)],
+    ),
+    "nc_gpuhash_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "nc_gpuhash_ctx_create": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
+    "nc_gpuhash_ctx_destroy": (None, [ctypes.c_void_p]),
+    "nc_gpuhash_submit": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+         ctypes.POINTER(ctypes.c_int)],
+    ),
+    "nc_gpuhash_submit_spans": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(NcKeySpan), ctypes.c_uint32, ctypes.c_void_p,
+         ctypes.POINTER(ctypes.c_int)],
+    ),
+    "nc_gpuhash_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "nc_gpuhash_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "nc_hashkit_batch": (
+        ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    ),
+    # sharding / info
+    "nc_gpuhash_shard_bounds": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
+    "nc_gpuhash_device_count": (ctypes.c_int, []),
+    "nc_gpuhash_version": (ctypes.c_char_p, []),
+    # synthetic generator
+    "nc_synth_lengths_host": (
+        ctypes.c_int, [ctypes.POINTER(NcSynthSpec), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+    ),
+    "nc_synth_offsets_host": (
+        ctypes.c_int, [ctypes.POINTER(NcSynthSpec), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+    ),
+    "nc_synth_fill_host": (
+        ctypes.c_int,
+        [ctypes.POINTER(NcSynthSpec), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p],
+    ),
+    "nc_synth_offsets_device": (
+        ctypes.c_int,
+        [ctypes.POINTER(NcSynthSpec), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p],
+    ),
+    "nc_synth_fill_device": (
+        ctypes.c_int,
+        [ctypes.POINTER(NcSynthSpec), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p],
+    ),
+}
+
+
+class NcError(OSError):
+    """A C-ABI call returned NC_ERROR / NC_ENOMEM / NC_EAGAIN."""
+
+
+def lib() -> ctypes.CDLL:
+    """Load libnc_gpuhash.so once; raise if it has not been built."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                    "(the batched hasher has no CPU fallback)"
+                )
+            handle = ctypes.CDLL(LIB_PATH, use_errno=True)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+        return _lib
+
+
+def check(rc: int, what: str) -> None:
+    """Raise NcError for a non-NC_OK status, with the C errno."""
+    if rc != NC_OK:
+        err = ctypes.get_errno()
+        raise NcError(err, f"{what} failed: rstatus {rc} ({os.strerror(err) if err else 'no errno'})")

@@ -1,0 +1,379 @@
+/*
+ * Host side of the batched hasher, in C like the rest of twemproxy.
+ *
+ *  - hash: selector (src/nc_conf.c:1738-1764 conf_set_hash over
+ *    hash_strings[] :23-27, HASH_CODEC src/hashkit/nc_hashkit.h:24-36);
+ *  - contexts: nslots batches in flight, each with pinned host staging, its
+ *    own HIP stream and device buffers. submit() packs (copies) keys out of the
+ *    caller's mbuf spans into pinned staging — mbufs are recycled once the
+ *    message is released (src/nc_mbuf.c:118-128) — and enqueues H2D, the
+ *    kernel (nc_gpuhash_batch_device) and D2H without blocking; poll() is the
+ *    completion check the event loop (src/nc_core.c:356 core_loop) would call;
+ *  - byte-balanced shard planning for multi-GPU runs.
+ *
+ * There is no CPU fallback anywhere in this file: without a usable GPU every
+ * batched call fails with NC_ERROR / errno ENODEV.
+ */
+#include <errno.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "nc_gpuhash.h"
+
+/* ---------------- hash: selector ---------------- */
+
+static const char *const nc_mode_names[NC_GPUHASH_NMODES] = {
+    "one_at_a_time", "md5", "crc16", "crc32", "crc32a", "fnv1_64",
+    "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur", "jenkins",
+};
+
+int nc_gpuhash_mode_from_name(const char *name, size_t len)
+{
+    if (name != NULL) {
+        for (int m = 0; m < NC_GPUHASH_NMODES; m++) {
+            /* string_compare: equal length and bytes (src/nc_string.c) */
+            if (strlen(nc_mode_names[m]) == len && memcmp(nc_mode_names[m], name, len) == 0) {
+                return m;
+            }
+        }
+    }
+    errno = EINVAL; /* "is not a valid hash" */
+    return -1;
+}
+
+const char *nc_gpuhash_mode_name(int mode)
+{
+    if (mode < 0 || mode >= NC_GPUHASH_NMODES) {
+        return NULL;
+    }
+    return nc_mode_names[mode];
+}
+
+const char *nc_gpuhash_version(void) { return "nc_gpuhash 0.1.0 (gfx950)"; }
+
+int nc_gpuhash_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        return 0;
+    }
+    return n;
+}
+
+/* ---------------- shard planning ---------------- */
+
+rstatus_t nc_gpuhash_shard_bounds(const uint64_t *offsets, uint64_t nkeys, uint32_t nshards,
+                                  uint64_t *key_bounds)
+{
+    if (offsets == NULL || key_bounds == NULL || nshards == 0) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    const uint64_t base = offsets[0], total = offsets[nkeys] - offsets[0];
+    key_bounds[0] = 0;
+    for (uint32_t g = 1; g < nshards; g++) {
+        /* first key whose start is >= the g-th byte quantile; ranges with no
+         * bytes at all (all-empty keys) fall back to an even key split */
+        uint64_t cut;
+        if (total == 0) {
+            cut = nkeys * g / nshards;
+        } else {
+            unsigned __int128 want = (unsigned __int128)total * g / nshards;
+            uint64_t target = base + (uint64_t)want;
+            uint64_t lo = 0, hi = nkeys;
+            while (lo < hi) {
+                uint64_t mid = lo + (hi - lo) / 2;
+                if (offsets[mid] < target) lo = mid + 1; else hi = mid;
+            }
+            cut = lo;
+        }
+        if (cut < key_bounds[g - 1]) cut = key_bounds[g - 1];
+        key_bounds[g] = cut;
+    }
+    key_bounds[nshards] = nkeys;
+    return NC_OK;
+}
+
+/* ---------------- contexts ---------------- */
+
+struct nc_slot {
+    hipStream_t stream;
+    hipEvent_t done;
+    uint8_t *h_keys;
+    uint64_t *h_off;
+    uint32_t *h_out;
+    uint8_t *d_keys;
+    uint64_t *d_off;
+    uint32_t *d_out;
+    uint32_t *user_out;
+    uint32_t nkeys;
+    int busy;
+    int ticket;
+};
+
+struct nc_gpuhash_ctx {
+    int device;
+    uint64_t max_keys;
+    uint64_t max_key_bytes;
+    int nslots;
+    int next_gen;
+    struct nc_slot *slots;
+};
+
+static rstatus_t hip_fail(hipError_t e)
+{
+    errno = (e == hipErrorNoDevice || e == hipErrorInvalidDevice) ? ENODEV
+          : (e == hipErrorOutOfMemory ? ENOMEM : EIO);
+    return errno == ENOMEM ? NC_ENOMEM : NC_ERROR;
+}
+
+void nc_gpuhash_ctx_destroy(nc_gpuhash_ctx_t *ctx)
+{
+    if (ctx == NULL) {
+        return;
+    }
+    if (ctx->slots != NULL) {
+        hipSetDevice(ctx->device);
+        for (int i = 0; i < ctx->nslots; i++) {
+            struct nc_slot *s = &ctx->slots[i];
+            if (s->stream) hipStreamSynchronize(s->stream);
+            if (s->done) hipEventDestroy(s->done);
+            if (s->stream) hipStreamDestroy(s->stream);
+            if (s->h_keys) hipHostFree(s->h_keys);
+            if (s->h_off) hipHostFree(s->h_off);
+            if (s->h_out) hipHostFree(s->h_out);
+            if (s->d_keys) hipFree(s->d_keys);
+            if (s->d_off) hipFree(s->d_off);
+            if (s->d_out) hipFree(s->d_out);
+        }
+        free(ctx->slots);
+    }
+    free(ctx);
+}
+
+nc_gpuhash_ctx_t *nc_gpuhash_ctx_create(int device, uint64_t max_keys, uint64_t max_key_bytes, int nslots)
+{
+    if (max_keys == 0 || nslots < 1 || nslots > 64) {
+        errno = EINVAL;
+        return NULL;
+    }
+    int ndev = nc_gpuhash_device_count();
+    if (device < 0 || device >= ndev) {
+        errno = ENODEV;
+        return NULL;
+    }
+    nc_gpuhash_ctx_t *ctx = calloc(1, sizeof(*ctx));
+    if (ctx == NULL) {
+        errno = ENOMEM;
+        return NULL;
+    }
+    ctx->device = device;
+    ctx->max_keys = max_keys;
+    ctx->max_key_bytes = max_key_bytes;
+    ctx->nslots = nslots;
+    ctx->slots = calloc((size_t)nslots, sizeof(struct nc_slot));
+    if (ctx->slots == NULL || hipSetDevice(device) != hipSuccess) {
+        nc_gpuhash_ctx_destroy(ctx);
+        errno = ENOMEM;
+        return NULL;
+    }
+    const size_t kb = (size_t)max_key_bytes + NC_GPUHASH_PAD;
+    for (int i = 0; i < nslots; i++) {
+        struct nc_slot *s = &ctx->slots[i];
+        hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&s->h_keys, kb, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&s->h_off, (max_keys + 1) * sizeof(uint64_t), hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&s->h_out, max_keys * sizeof(uint32_t), hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc((void **)&s->d_keys, kb);
+        if (e == hipSuccess) e = hipMalloc((void **)&s->d_off, (max_keys + 1) * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMalloc((void **)&s->d_out, max_keys * sizeof(uint32_t));
+        if (e != hipSuccess) {
+            hip_fail(e);
+            int saved = errno;
+            nc_gpuhash_ctx_destroy(ctx);
+            errno = saved;
+            return NULL;
+        }
+        s->ticket = -1;
+    }
+    return ctx;
+}
+
+/* Copy a finished slot's hashes to the caller and free the slot. */
+static void slot_finish(struct nc_slot *s)
+{
+    memcpy(s->user_out, s->h_out, (size_t)s->nkeys * sizeof(uint32_t));
+    s->busy = 0;
+}
+
+static struct nc_slot *slot_acquire(nc_gpuhash_ctx_t *ctx, int *idx)
+{
+    for (int i = 0; i < ctx->nslots; i++) {
+        struct nc_slot *s = &ctx->slots[i];
+        if (s->busy && hipEventQuery(s->done) == hipSuccess) {
+            slot_finish(s);
+        }
+        if (!s->busy) {
+            *idx = i;
+            return s;
+        }
+    }
+    return NULL;
+}
+
+/* Enqueue H2D -> kernel -> D2H on the slot's stream; staging already packed. */
+static rstatus_t slot_launch(nc_gpuhash_ctx_t *ctx, struct nc_slot *s, int idx, int mode, uint32_t nkeys,
+                             uint32_t *out, int *ticket)
+{
+    const uint64_t nbytes = s->h_off[nkeys];
+    memset(s->h_keys + nbytes, 0, NC_GPUHASH_PAD);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipMemcpyAsync(s->d_keys, s->h_keys, nbytes + NC_GPUHASH_PAD, hipMemcpyHostToDevice, s->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s->d_off, s->h_off, ((size_t)nkeys + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    if (nc_gpuhash_batch_device(mode, s->d_keys, s->d_off, nkeys, s->d_out, s->stream) != NC_OK) return NC_ERROR;
+    e = hipMemcpyAsync(s->h_out, s->d_out, (size_t)nkeys * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipEventRecord(s->done, s->stream);
+    if (e != hipSuccess) return hip_fail(e);
+    s->user_out = out;
+    s->nkeys = nkeys;
+    s->busy = 1;
+    s->ticket = idx + ctx->nslots * (ctx->next_gen++ & 0xffffff);
+    *ticket = s->ticket;
+    return NC_OK;
+}
+
+rstatus_t nc_gpuhash_submit(nc_gpuhash_ctx_t *ctx, int mode, const uint8_t *keys, const uint64_t *offsets,
+                            uint32_t nkeys, uint32_t *out, int *ticket)
+{
+    if (ctx == NULL || offsets == NULL || out == NULL || ticket == NULL || mode < 0 || mode >= NC_GPUHASH_NMODES) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    const uint64_t nbytes = offsets[nkeys] - offsets[0];
+    if (nkeys > ctx->max_keys || nbytes > ctx->max_key_bytes) {
+        errno = ENOMEM;
+        return NC_ENOMEM;
+    }
+    int idx;
+    struct nc_slot *s = slot_acquire(ctx, &idx);
+    if (s == NULL) {
+        errno = EAGAIN;
+        return NC_EAGAIN;
+    }
+    if (nbytes) memcpy(s->h_keys, keys + offsets[0], nbytes);
+    const uint64_t base = offsets[0];
+    for (uint32_t i = 0; i <= nkeys; i++) {
+        s->h_off[i] = offsets[i] - base;
+    }
+    return slot_launch(ctx, s, idx, mode, nkeys, out, ticket);
+}
+
+rstatus_t nc_gpuhash_submit_spans(nc_gpuhash_ctx_t *ctx, int mode, const struct nc_keyspan *spans,
+                                  uint32_t nkeys, uint32_t *out, int *ticket)
+{
+    if (ctx == NULL || (spans == NULL && nkeys) || out == NULL || ticket == NULL || mode < 0 ||
+        mode >= NC_GPUHASH_NMODES) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    if (nkeys > ctx->max_keys) {
+        errno = ENOMEM;
+        return NC_ENOMEM;
+    }
+    int idx;
+    struct nc_slot *s = slot_acquire(ctx, &idx);
+    if (s == NULL) {
+        errno = EAGAIN;
+        return NC_EAGAIN;
+    }
+    uint64_t pos = 0;
+    s->h_off[0] = 0;
+    for (uint32_t i = 0; i < nkeys; i++) {
+        const size_t n = (size_t)(spans[i].end - spans[i].start);
+        if (pos + n > ctx->max_key_bytes) {
+            errno = ENOMEM;
+            return NC_ENOMEM;
+        }
+        memcpy(s->h_keys + pos, spans[i].start, n);
+        pos += n;
+        s->h_off[i + 1] = pos;
+    }
+    return slot_launch(ctx, s, idx, mode, nkeys, out, ticket);
+}
+
+static struct nc_slot *slot_of(nc_gpuhash_ctx_t *ctx, int ticket)
+{
+    if (ctx == NULL || ticket < 0) return NULL;
+    return &ctx->slots[ticket % ctx->nslots];
+}
+
+rstatus_t nc_gpuhash_poll(nc_gpuhash_ctx_t *ctx, int ticket)
+{
+    struct nc_slot *s = slot_of(ctx, ticket);
+    if (s == NULL) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    if (!s->busy || s->ticket != ticket) {
+        return NC_OK; /* finished and already delivered */
+    }
+    hipError_t e = hipEventQuery(s->done);
+    if (e == hipErrorNotReady) return NC_EAGAIN;
+    if (e != hipSuccess) return hip_fail(e);
+    slot_finish(s);
+    return NC_OK;
+}
+
+rstatus_t nc_gpuhash_wait(nc_gpuhash_ctx_t *ctx, int ticket)
+{
+    struct nc_slot *s = slot_of(ctx, ticket);
+    if (s == NULL) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    if (!s->busy || s->ticket != ticket) return NC_OK;
+    hipError_t e = hipEventSynchronize(s->done);
+    if (e != hipSuccess) return hip_fail(e);
+    slot_finish(s);
+    return NC_OK;
+}
+
+/* ---------------- process-wide synchronous batch ---------------- */
+
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+static nc_gpuhash_ctx_t *g_ctx;
+
+rstatus_t nc_hashkit_batch(int mode, const uint8_t *keys, const uint64_t *offsets, uint32_t nkeys, uint32_t *out)
+{
+    if (offsets == NULL || out == NULL || mode < 0 || mode >= NC_GPUHASH_NMODES) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    const uint64_t nbytes = offsets[nkeys] - offsets[0];
+    pthread_mutex_lock(&g_lock);
+    if (g_ctx == NULL || g_ctx->max_keys < nkeys || g_ctx->max_key_bytes < nbytes) {
+        uint64_t mk = nkeys < 65536 ? 65536 : nkeys, mb = nbytes < (1u << 22) ? (1u << 22) : nbytes;
+        if (g_ctx) {
+            if (g_ctx->max_keys > mk) mk = g_ctx->max_keys;
+            if (g_ctx->max_key_bytes > mb) mb = g_ctx->max_key_bytes;
+            nc_gpuhash_ctx_destroy(g_ctx);
+        }
+        g_ctx = nc_gpuhash_ctx_create(0, mk, mb, 1);
+        if (g_ctx == NULL) {
+            int saved = errno;
+            pthread_mutex_unlock(&g_lock);
+            errno = saved;
+            return saved == ENOMEM ? NC_ENOMEM : NC_ERROR;
+        }
+    }
+    int ticket;
+    rstatus_t rc = nc_gpuhash_submit(g_ctx, mode, keys, offsets, nkeys, out, &ticket);
+    if (rc == NC_OK) rc = nc_gpuhash_wait(g_ctx, ticket);
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}

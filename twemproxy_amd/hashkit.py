@@ -1,0 +1,322 @@
+"""Python mirror of twemproxy's hashkit interface over the MI355X batched hasher.
+
+Names follow the reference: the 12 modes of HASH_CODEC
+(src/hashkit/nc_hashkit.h:24-36), ``conf_set_hash`` (src/nc_conf.c:1738-1764)
+for the per-pool ``hash:`` selector, ``hash_<name>`` per-key functions.
+Batched calls go through the C ABI (libnc_gpuhash.so) into the gfx950
+kernels; they raise ``NcError`` when no GPU is usable instead of falling back.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+# HASH_CODEC order == hash_type_t values (src/hashkit/nc_hashkit.h:24-48).
+HASH_NAMES = (
+    "one_at_a_time", "md5", "crc16", "crc32", "crc32a", "fnv1_64",
+    "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur", "jenkins",
+)
+HASH_DEFAULT = "fnv1a_64"  # CONF_DEFAULT_HASH, src/nc_conf.h:44
+NMODES = len(HASH_NAMES)
+
+# DIST_CODEC (src/hashkit/nc_hashkit.h:38-41)
+DIST_NAMES = ("ketama", "modula", "random")
+
+
+def conf_set_hash(value: str | bytes) -> int:
+    """``hash:`` string -> hash_type_t, through the C selector.
+
+    Raises ValueError("is not a valid hash") like conf_set_hash's error string.
+    """
+    raw = value.encode() if isinstance(value, str) else bytes(value)
+    mode = L.lib().nc_gpuhash_mode_from_name(raw, len(raw))
+    if mode < 0:
+        raise ValueError(f"'{raw.decode(errors='replace')}' is not a valid hash")
+    return mode
+
+
+def mode_of(hash_: int | str) -> int:
+    if isinstance(hash_, int):
+        if not 0 <= hash_ < NMODES:
+            raise ValueError(f"hash mode {hash_} out of range")
+        return hash_
+    return conf_set_hash(hash_)
+
+
+def hash_key(hash_: int | str, key: bytes) -> int:
+    """Per-key host hash through the link-compatible ``hash_<name>`` symbol."""
+    name = HASH_NAMES[mode_of(hash_)]
+    return int(getattr(L.lib(), "hash_" + name)(key, len(key)))
+
+
+def ketama_hash(key: bytes, alignment: int) -> int:
+    return int(L.lib().ketama_hash(key, len(key), alignment))
+
+
+def md5_signature(key: bytes) -> bytes:
+    buf = ctypes.create_string_buffer(16)
+    L.lib().md5_signature(key, len(key), buf)
+    return buf.raw
+
+
+# ---------------------------------------------------------------- CSR helpers
+
+
+def pack_keys(keys: Sequence[bytes], pad: int = L.NC_GPUHASH_PAD) -> tuple[np.ndarray, np.ndarray]:
+    """List of keys -> (uint8 byte stream padded by `pad`, uint64 offsets[n+1])."""
+    lens = np.fromiter((len(k) for k in keys), dtype=np.uint64, count=len(keys))
+    offsets = np.zeros(len(keys) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    buf = np.zeros(int(offsets[-1]) + pad, dtype=np.uint8)
+    if len(keys):
+        buf[: int(offsets[-1])] = np.frombuffer(b"".join(keys), dtype=np.uint8)
+    return buf, offsets
+
+
+def shard_bounds(offsets: np.ndarray, nshards: int) -> np.ndarray:
+    """Byte-balanced contiguous key ranges (nc_gpuhash_shard_bounds)."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = offsets.size - 1
+    out = np.zeros(nshards + 1, dtype=np.uint64)
+    L.check(
+        L.lib().nc_gpuhash_shard_bounds(offsets.ctypes.data, n, nshards, out.ctypes.data),
+        "nc_gpuhash_shard_bounds",
+    )
+    return out
+
+
+def device_count() -> int:
+    return int(L.lib().nc_gpuhash_device_count())
+
+
+# ---------------------------------------------------------------- batches
+
+
+def _stream_handle(stream) -> int | None:
+    if stream is None:
+        import torch
+
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def hash_batch_device(hash_: int | str, keys, offsets, out=None, stream=None):
+    """Device-resident batch on torch tensors.
+
+    keys: uint8 CUDA tensor readable NC_GPUHASH_PAD bytes past offsets[-1];
+    offsets: int64 CUDA tensor of n+1 non-decreasing offsets;
+    out: int32 CUDA tensor of n (allocated if None; the bits are the u32 hash).
+    Enqueued on `stream` (default: torch's current stream).
+    """
+    import torch
+
+    mode = mode_of(hash_)
+    n = offsets.numel() - 1
+    if keys.dtype != torch.uint8 or offsets.dtype != torch.int64:
+        raise TypeError("keys must be uint8 and offsets int64")
+    if not (keys.is_cuda and offsets.is_cuda):
+        raise ValueError("hash_batch_device needs CUDA (HIP) tensors")
+    if not (keys.is_contiguous() and offsets.is_contiguous()):
+        raise ValueError("keys and offsets must be contiguous")
+    if out is None:
+        out = torch.empty(max(n, 0), dtype=torch.int32, device=keys.device)
+    L.check(
+        L.lib().nc_gpuhash_batch_device(
+            mode, keys.data_ptr(), offsets.data_ptr(), n, out.data_ptr(), _stream_handle(stream)
+        ),
+        "nc_gpuhash_batch_device",
+    )
+    return out
+
+
+def time_batch_device(hash_: int | str, keys, offsets, out, iters: int, stream=None) -> float:
+    """Mean ms per launch over `iters` launches, timed by hipEvents on the launch stream."""
+    mode = mode_of(hash_)
+    ms = ctypes.c_float(0.0)
+    L.check(
+        L.lib().nc_gpuhash_time_device(
+            mode, keys.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, out.data_ptr(),
+            _stream_handle(stream), iters, ctypes.byref(ms),
+        ),
+        "nc_gpuhash_time_device",
+    )
+    return float(ms.value)
+
+
+def hash_batch_host(hash_: int | str, keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    """Synchronous host batch (nc_hashkit_batch): pinned copy -> GPU -> copy back."""
+    mode = mode_of(hash_)
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = offsets.size - 1
+    out = np.empty(n, dtype=np.uint32)
+    L.check(
+        L.lib().nc_hashkit_batch(mode, keys.ctypes.data, offsets.ctypes.data, n, out.ctypes.data),
+        "nc_hashkit_batch",
+    )
+    return out
+
+
+def hash_keys(hash_: int | str, keys: Sequence[bytes]) -> list[int]:
+    """Batch-hash a list of keys on the GPU (host round trip)."""
+    buf, off = pack_keys(keys)
+    return [int(x) for x in hash_batch_host(hash_, buf, off)]
+
+
+class Context:
+    """nc_gpuhash_ctx: pinned, multi-slot asynchronous host batches."""
+
+    def __init__(self, device: int = 0, max_keys: int = 65536, max_key_bytes: int = 1 << 22, nslots: int = 2):
+        self._lib = L.lib()
+        handle = self._lib.nc_gpuhash_ctx_create(device, max_keys, max_key_bytes, nslots)
+        if not handle:
+            err = ctypes.get_errno()
+            raise L.NcError(err, "nc_gpuhash_ctx_create failed")
+        self._h = handle
+        self._keep: dict[int, tuple] = {}
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.nc_gpuhash_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def submit(self, hash_: int | str, keys: np.ndarray, offsets: np.ndarray) -> tuple[int, np.ndarray]:
+        """Returns (ticket, out); `out` is valid once poll()/wait() says NC_OK."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = offsets.size - 1
+        out = np.empty(n, dtype=np.uint32)
+        ticket = ctypes.c_int(-1)
+        rc = self._lib.nc_gpuhash_submit(
+            self._h, mode_of(hash_), keys.ctypes.data, offsets.ctypes.data, n, out.ctypes.data, ctypes.byref(ticket)
+        )
+        if rc == L.NC_EAGAIN:
+            raise BlockingIOError("all context slots busy")
+        L.check(rc, "nc_gpuhash_submit")
+        self._keep[ticket.value] = (out,)
+        return ticket.value, out
+
+    def submit_spans(self, hash_: int | str, buf: np.ndarray, spans: Sequence[tuple[int, int]]) -> tuple[int, np.ndarray]:
+        """Spans are (start, end) byte offsets into `buf` (keypos-style borrowed keys)."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        base = buf.ctypes.data
+        arr = (L.NcKeySpan * max(len(spans), 1))()
+        for i, (s, e) in enumerate(spans):
+            arr[i].start = base + s
+            arr[i].end = base + e
+        out = np.empty(len(spans), dtype=np.uint32)
+        ticket = ctypes.c_int(-1)
+        rc = self._lib.nc_gpuhash_submit_spans(
+            self._h, mode_of(hash_), arr, len(spans), out.ctypes.data, ctypes.byref(ticket)
+        )
+        if rc == L.NC_EAGAIN:
+            raise BlockingIOError("all context slots busy")
+        L.check(rc, "nc_gpuhash_submit_spans")
+        self._keep[ticket.value] = (out,)
+        return ticket.value, out
+
+    def poll(self, ticket: int) -> bool:
+        rc = self._lib.nc_gpuhash_poll(self._h, ticket)
+        if rc == L.NC_EAGAIN:
+            return False
+        L.check(rc, "nc_gpuhash_poll")
+        self._keep.pop(ticket, None)
+        return True
+
+    def wait(self, ticket: int) -> None:
+        L.check(self._lib.nc_gpuhash_wait(self._h, ticket), "nc_gpuhash_wait")
+        self._keep.pop(ticket, None)
+
+
+# ---------------------------------------------------------------- synthetic keys
+
+SYNTH_FIXED, SYNTH_ZIPF, SYNTH_UNIFORM = 0, 1, 2
+BYTES_FULL, BYTES_PRINTABLE = 0, 1
+
+
+@dataclass(frozen=True)
+class SynthSpec:
+    """Synthetic key set of SURVEY.md §8d (include/nc_gpuhash_synth.h)."""
+
+    seed: int
+    len_dist: int = SYNTH_FIXED
+    len_a: int = 16
+    len_b: int = 16
+    charset: int = BYTES_FULL
+    zipf_s: float = 1.0
+
+    def c(self) -> L.NcSynthSpec:
+        return L.NcSynthSpec(self.seed, self.len_dist, self.len_a, self.len_b, self.charset, self.zipf_s)
+
+    @staticmethod
+    def fixed(seed: int, length: int, charset: int = BYTES_FULL) -> "SynthSpec":
+        return SynthSpec(seed, SYNTH_FIXED, length, length, charset)
+
+    @staticmethod
+    def zipf(seed: int, lmin: int = 8, nvals: int = 57, s: float = 1.0, charset: int = BYTES_FULL) -> "SynthSpec":
+        """len = lmin - 1 + r, r in [1, nvals], P(r) ~ 1/r^s (C2: 8..64 B)."""
+        return SynthSpec(seed, SYNTH_ZIPF, lmin, nvals, charset, s)
+
+    @staticmethod
+    def uniform(seed: int, lo: int, hi: int, charset: int = BYTES_FULL) -> "SynthSpec":
+        return SynthSpec(seed, SYNTH_UNIFORM, lo, hi, charset)
+
+
+# Configurations of BASELINE.json / SURVEY.md §8d.
+CONFIGS = {
+    "C1": dict(spec=SynthSpec.fixed(1, 16), nkeys=1 << 20, modes=("fnv1a_64",)),
+    "C2": dict(spec=SynthSpec.zipf(2), nkeys=1 << 26, modes=("fnv1a_64",)),
+    "C3": dict(spec=SynthSpec.fixed(3, 32), nkeys=1 << 26, modes=HASH_NAMES),
+    "C4": dict(spec=SynthSpec.fixed(4, 256), nkeys=1 << 28, modes=("md5", "crc32")),
+    "C5": dict(spec=SynthSpec.zipf(5, charset=BYTES_PRINTABLE), nkeys=64 * 128, modes=("fnv1a_64",)),
+}
+
+
+def synth_host(spec: SynthSpec, first: int, n: int, pad: int = L.NC_GPUHASH_PAD) -> tuple[np.ndarray, np.ndarray]:
+    """Keys [first, first+n) on the host: (uint8 bytes padded, uint64 offsets from 0)."""
+    lib = L.lib()
+    cs = spec.c()
+    off = np.empty(n + 1, dtype=np.uint64)
+    L.check(lib.nc_synth_offsets_host(ctypes.byref(cs), first, n, off.ctypes.data), "nc_synth_offsets_host")
+    buf = np.zeros(int(off[-1]) + pad, dtype=np.uint8)
+    L.check(lib.nc_synth_fill_host(ctypes.byref(cs), first, n, off.ctypes.data, buf.ctypes.data), "nc_synth_fill_host")
+    return buf, off
+
+
+def synth_device(spec: SynthSpec, first: int, n: int, device="cuda", pad: int = L.NC_GPUHASH_PAD, stream=None):
+    """Keys [first, first+n) generated on the GPU: (uint8 tensor padded, int64 offsets tensor)."""
+    import torch
+
+    lib = L.lib()
+    cs = spec.c()
+    off = torch.empty(n + 1, dtype=torch.int64, device=device)
+    st = _stream_handle(stream)
+    L.check(lib.nc_synth_offsets_device(ctypes.byref(cs), first, n, off.data_ptr(), st), "nc_synth_offsets_device")
+    total = int(off[-1].item())
+    keys = torch.zeros(total + pad, dtype=torch.uint8, device=device)
+    L.check(lib.nc_synth_fill_device(ctypes.byref(cs), first, n, off.data_ptr(), keys.data_ptr(), st),
+            "nc_synth_fill_device")
+    return keys, off
+
+
+def iter_modes(modes: Iterable[int | str]) -> list[int]:
+    return [mode_of(m) for m in modes]

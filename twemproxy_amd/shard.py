@@ -1,0 +1,85 @@
+"""Multi-GPU sharding of a key batch.
+
+Keys are independent, so a batch splits into contiguous, byte-balanced key
+ranges — one per rank — and each rank hashes its range with no exchange. The
+only collective is the ingest scatter from a root rank: RCCL has no
+variable-size scatter, so the root issues grouped point-to-point sends (one
+``ncclSend`` of offsets and one of key bytes per peer inside a group, i.e.
+``torch.distributed.batch_isend_irecv`` on the ``nccl`` backend), which use
+the root's direct xGMI links to all peers in parallel. The same code runs on
+the ``gloo`` backend with CPU tensors for the CPU tests.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ._lib import NC_GPUHASH_PAD
+
+
+def plan_bounds(offsets: torch.Tensor, nshards: int) -> torch.Tensor:
+    """Key bounds (nshards + 1, int64) splitting offsets' bytes evenly.
+
+    Cut g is the first key whose start offset is >= g/nshards of the bytes —
+    the same lower-bound rule as nc_gpuhash_shard_bounds (host C); computed
+    with searchsorted on whatever device `offsets` lives on.
+    """
+    n = offsets.numel() - 1
+    base = offsets[0]
+    total = offsets[-1] - base
+    g = torch.arange(1, nshards, device=offsets.device, dtype=torch.int64)
+    if int(total) == 0:
+        cuts = (g * n) // nshards
+    else:
+        # total * g / nshards without int64 overflow for multi-GiB batches
+        q, r = total // nshards, total % nshards
+        targets = base + q * g + (r * g) // nshards
+        cuts = torch.searchsorted(offsets[:n].contiguous(), targets, right=False)
+        cuts = torch.cummax(cuts, 0).values
+    zero = torch.zeros(1, dtype=torch.int64, device=offsets.device)
+    end = torch.full((1,), n, dtype=torch.int64, device=offsets.device)
+    return torch.cat([zero, cuts.to(torch.int64), end])
+
+
+def scatter_shards(keys: torch.Tensor | None, offsets: torch.Tensor | None, device: torch.device,
+                   root: int = 0, group=None, pad: int = NC_GPUHASH_PAD):
+    """Scatter byte-balanced key ranges from `root` to every rank.
+
+    keys/offsets: the full batch on the root (uint8 bytes, int64 offsets),
+    ignored elsewhere. Returns (local_keys uint8 padded by `pad`,
+    local_offsets int64 rebased to 0, first_key_index) on `device`.
+    """
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    meta = torch.zeros(2 * (world + 1), dtype=torch.int64, device=device)
+    if rank == root:
+        kb = plan_bounds(offsets, world)
+        bb = offsets[kb]
+        meta.copy_(torch.cat([kb, bb]).to(device))
+    dist.broadcast(meta, src=root, group=group)
+    kb = meta[: world + 1].tolist()
+    bb = meta[world + 1:].tolist()
+    klo, khi, blo, bhi = kb[rank], kb[rank + 1], bb[rank], bb[rank + 1]
+
+    local_keys = torch.zeros(bhi - blo + pad, dtype=torch.uint8, device=device)
+    local_off = torch.empty(khi - klo + 1, dtype=torch.int64, device=device)
+    ops = []
+    if rank == root:
+        for r in range(world):
+            rk0, rk1, rb0, rb1 = kb[r], kb[r + 1], bb[r], bb[r + 1]
+            if r == root:
+                local_keys[: bhi - blo].copy_(keys[blo:bhi])
+                local_off.copy_(offsets[klo: khi + 1])
+                continue
+            ops.append(dist.P2POp(dist.isend, offsets[rk0: rk1 + 1].contiguous(), r, group))
+            if rb1 > rb0:
+                ops.append(dist.P2POp(dist.isend, keys[rb0:rb1].contiguous(), r, group))
+    else:
+        ops.append(dist.P2POp(dist.irecv, local_off, root, group))
+        if bhi > blo:
+            ops.append(dist.P2POp(dist.irecv, local_keys[: bhi - blo], root, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    local_off -= blo
+    return local_keys, local_off, klo
