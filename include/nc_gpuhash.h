@@ -99,10 +99,14 @@ rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, const uint64_t
                                  uint64_t nkeys, uint32_t *d_out, void *stream,
                                  int iters, float *avg_ms);
 
-/* Launch tuning (process-wide; for tests and benchmarks). grid_cap: maximum
- * workgroups per launch (0 = one per 256-key tile, -1 = keep). sort: group a
- * tile's keys by length class before hashing (1 on, 0 off, -1 keep). */
-rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort);
+/* Launch tuning (process-wide; for tests and benchmarks; every setting gives
+ * identical outputs). grid_cap: maximum workgroups per launch (0 = persistent,
+ * one per resident slot; -1 = keep). sort: group a tile's keys by length
+ * before hashing (1 on, 0 off, -1 keep). variant: kernel code variant bits
+ * (bit 0: shift-add FNV-64 multiply; bits 1-2: L2 prefetch distance code,
+ * 0 off, 1..3 = 2..4 tiles ahead; bit 3: DIAGNOSTIC no-hash build, fnv1a_64
+ * unsorted only, outputs are NOT hashes; -1 = keep). */
+rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
 /* ---- 3b. host batches through a context (pinned staging, one stream per slot) ---- */
 typedef struct nc_gpuhash_ctx nc_gpuhash_ctx_t;

@@ -72,7 +72,7 @@ SIGNATURES = {
         [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
          ctypes.c_int, ctypes.POINTER(ctypes.c_float)],
     ),
-    "nc_gpuhash_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "nc_gpuhash_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "nc_gpuhash_ctx_create": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
     "nc_gpuhash_ctx_destroy": (None, [ctypes.c_void_p]),
     "nc_gpuhash_submit": (
@@ -94,6 +94,12 @@ SIGNATURES = {
     "nc_gpuhash_shard_bounds": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
     "nc_gpuhash_device_count": (ctypes.c_int, []),
     "nc_gpuhash_version": (ctypes.c_char_p, []),
+    # diagnostics (include/nc_gpuhash_probe.h)
+    "nc_gpuhash_probe_read": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+         ctypes.POINTER(ctypes.c_float)],
+    ),
     # synthetic generator
     "nc_synth_lengths_host": (
         ctypes.c_int, [ctypes.POINTER(NcSynthSpec), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
@@ -131,6 +137,13 @@ def lib() -> ctypes.CDLL:
                     f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                     "(the batched hasher has no CPU fallback)"
                 )
+            # torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's).
+            # Load it first so this process has ONE HIP runtime, shared by torch
+            # and libnc_gpuhash.so; if ours came first, torch's HIP init fails.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             handle = ctypes.CDLL(LIB_PATH, use_errno=True)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(handle, name)

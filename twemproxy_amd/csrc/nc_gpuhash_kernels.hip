@@ -37,65 +37,81 @@ namespace {
 
 constexpr int kBlock = 256;                  /* threads per workgroup = keys per tile */
 constexpr int kTile = kBlock;
-constexpr uint32_t kSlabCap = 16384 + 208;    /* staged key bytes per tile: 8 workgroups fit one CU (160 KiB) */
-constexpr int kStageIters = (kSlabCap / 16 + kBlock - 1) / kBlock;
 constexpr int kBuckets = 64;
+constexpr uint32_t kLdsBudget = 20480;        /* 8 workgroups per CU (160 KiB LDS) */
+constexpr uint32_t kRing = 8;                /* slab-bounds ring slots (tiles t .. t+5 in use) */
+constexpr uint32_t kDumpBytes = 256;          /* landing area of the L2-prefetch DMA (never read) */
+constexpr uint32_t kSmall = 4 * kTile + 2 * kTile + 8 * kBuckets + 16 + 4 * 256 + 16 * kRing + kDumpBytes;
+constexpr uint32_t kSlabCap = ((kLdsBudget - kSmall) / 2) & ~15u; /* per slab buffer (double buffered) */
+constexpr int kStageIters = (kSlabCap / 16 + kBlock - 1) / kBlock;
 
 /* LDS carve (one __shared__ array, all offsets 16-byte aligned) */
-constexpr uint32_t kOffSlab = 0;
-constexpr uint32_t kOffStart = kOffSlab + kSlabCap;            /* u32[kTile] key start in slab */
-constexpr uint32_t kOffLen = kOffStart + 4 * kTile;            /* u32[kTile] key length */
-constexpr uint32_t kOffPerm = kOffLen + 4 * kTile;             /* u16[kTile] sorted -> tile index */
-constexpr uint32_t kOffHist = kOffPerm + 2 * kTile;            /* u32[kBuckets] */
-constexpr uint32_t kOffFlag = kOffHist + 4 * kBuckets;         /* u32[4] */
+constexpr uint32_t kOffSlab0 = 0;
+constexpr uint32_t kOffSlab1 = kSlabCap;
+constexpr uint32_t kOffKey = 2 * kSlabCap;                     /* u32[kTile] key start | length << 16 */
+constexpr uint32_t kOffPerm = kOffKey + 4 * kTile;             /* u16[kTile] sorted -> tile index */
+constexpr uint32_t kOffHist = kOffPerm + 2 * kTile;            /* u32[2][kBuckets] */
+constexpr uint32_t kOffFlag = kOffHist + 8 * kBuckets;         /* u32[2] (+pad) */
 constexpr uint32_t kOffTab = kOffFlag + 16;                    /* u32[256] crc table */
-constexpr uint32_t kSmemBytes = kOffTab + 4 * 256;
+constexpr uint32_t kOffRing = kOffTab + 4 * 256;               /* u64[kRing][2] slab bounds {S, E} */
+constexpr uint32_t kOffDump = kOffRing + 16 * kRing;           /* prefetch landing area */
+constexpr uint32_t kSmemBytes = kOffDump + kDumpBytes;
 
+static_assert(kSmemBytes <= kLdsBudget, "LDS budget");
+static_assert(kSlabCap >= 8192 + 48, "a 256 x 32 B tile must fit one slab buffer");
+static_assert(kSlabCap < 65536, "sorted key positions are packed in 16 bits");
 static_assert(kOffTab % 16 == 0, "LDS carve must stay 16-byte aligned");
 
 /* ---------------- realigning readers ---------------- */
 
 struct LdsSrc {
     typedef uint32_t pos_t;
-    const uint8_t *base;
-    __device__ __forceinline__ uint2 q(uint32_t i) const { return reinterpret_cast<const uint2 *>(base)[i]; }
+    const uint32_t *base; /* 16-byte aligned LDS slab, read as dwords */
+    /* dwords i, i+1 (4-byte aligned): one ds_read2_b32 */
+    __device__ __forceinline__ uint2 d2(uint32_t i) const { return make_uint2(base[i], base[i + 1]); }
+    __device__ __forceinline__ uint32_t d1(uint32_t i) const { return base[i]; }
 };
 
 struct GlobalSrc {
     typedef uint64_t pos_t;
-    const uint8_t *base;
-    __device__ __forceinline__ uint2 q(uint64_t i) const { return reinterpret_cast<const uint2 *>(base)[i]; }
+    const uint32_t *base; /* 16-byte aligned key buffer */
+    __device__ __forceinline__ uint2 d2(uint64_t i) const { return make_uint2(base[i], base[i + 1]); }
+    __device__ __forceinline__ uint32_t d1(uint64_t i) const { return base[i]; }
 };
 
 /* Sequential little-endian words of a byte string starting at any byte
- * position p: two aligned 8-byte reads are funnel-shifted with v_alignbyte. */
+ * position p: aligned dwords funnel-shifted by (p & 3) bytes with
+ * v_alignbyte_b32; one ds_read2_b32 per 8 bytes, no selects. Reads at most
+ * 14 bytes past the end of the string (covered by the staged look-ahead
+ * piece / NC_GPUHASH_PAD). */
 template <class Src>
 struct QStream {
     Src src;
-    typename Src::pos_t qi;
-    uint32_t sel;   /* (p & 7) >= 4 */
-    uint32_t sh;    /* p & 3 */
-    uint2 cur;
+    typename Src::pos_t di;
+    uint32_t sh;
+    uint32_t prev;
+    uint2 ahead; /* dwords di+1, di+2, read one step early */
 
     __device__ __forceinline__ void init(const Src &s, typename Src::pos_t p)
     {
         src = s;
-        qi = p >> 3;
-        sel = ((uint32_t)p >> 2) & 1u;
+        di = p >> 2;
         sh = (uint32_t)p & 3u;
-        cur = src.q(qi);
+        prev = src.d1(di);
+        ahead = src.d2(di + 1);
     }
-    /* next 8 bytes as two words */
+    /* next 8 bytes as two words; the read for the following 8 is issued now
+     * (it may touch up to 22 bytes past the string: inside the staged
+     * look-ahead piece / NC_GPUHASH_PAD) */
     __device__ __forceinline__ uint2 next8()
     {
-        uint2 nx = src.q(++qi);
-        uint32_t a = sel ? cur.y : cur.x;
-        uint32_t b = sel ? nx.x : cur.y;
-        uint32_t c = sel ? nx.y : nx.x;
+        const uint2 d = ahead;
+        di += 2;
+        ahead = src.d2(di + 1);
         uint2 r;
-        r.x = __builtin_amdgcn_alignbyte(b, a, sh);
-        r.y = __builtin_amdgcn_alignbyte(c, b, sh);
-        cur = nx;
+        r.x = __builtin_amdgcn_alignbyte(d.x, prev, sh);
+        r.y = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
+        prev = d.y;
         return r;
     }
 };
@@ -141,9 +157,34 @@ __device__ __forceinline__ uint32_t byte_init()
     return 0u; /* one_at_a_time, crc16 */
 }
 
-template <int MODE>
-__device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t b, const uint32_t *tab)
+/* Shift counts the compiler cannot see through: with them, (h << s1) + h
+ * stays three full-rate v_lshl_add_u32 (3h, 27h, 435h = h * 0x1b3) instead of
+ * being folded back into the multi-pass v_mul_lo_u32, and — unlike inline asm
+ * — the instructions stay visible to the scheduler and hazard recognizer. */
+struct ShiftK {
+    uint32_t s1, s3, s4;
+};
+__device__ __forceinline__ ShiftK opaque_shifts()
 {
+    ShiftK k;
+    asm volatile("s_mov_b32 %0, 1" : "=s"(k.s1));
+    asm volatile("s_mov_b32 %0, 3" : "=s"(k.s3));
+    asm volatile("s_mov_b32 %0, 4" : "=s"(k.s4));
+    return k;
+}
+__device__ __forceinline__ uint32_t mul_0x1b3(uint32_t h, const ShiftK &k)
+{
+    const uint32_t t3 = (h << k.s1) + h;
+    const uint32_t t27 = (t3 << k.s3) + t3;
+    return (t27 << k.s4) + t3;
+}
+
+/* VAR bit 0: FNV-64-truncated multiply by shift-adds. */
+template <int MODE, int VAR = 0>
+__device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t b, const uint32_t *tab, const ShiftK &k)
+{
+    if constexpr (MODE == NC_GPUHASH_FNV1A_64 && (VAR & 1)) return mul_0x1b3(h ^ nc_sx8(b), k);
+    if constexpr (MODE == NC_GPUHASH_FNV1_64 && (VAR & 1)) return mul_0x1b3(h, k) ^ nc_sx8(b);
     if constexpr (MODE == NC_GPUHASH_FNV1A_64) return nc_fnv1a_64_step(h, b);
     if constexpr (MODE == NC_GPUHASH_FNV1_64) return nc_fnv1_64_step(h, b);
     if constexpr (MODE == NC_GPUHASH_FNV1_32) return nc_fnv1_32_step(h, b);
@@ -163,38 +204,41 @@ __device__ __forceinline__ uint32_t byte_final(uint32_t h)
     return h;
 }
 
-template <int MODE>
-__device__ __forceinline__ uint32_t word_bytes(uint32_t h, uint32_t w, const uint32_t *tab)
+template <int MODE, int VAR>
+__device__ __forceinline__ uint32_t word_bytes(uint32_t h, uint32_t w, const uint32_t *tab, const ShiftK &k)
 {
-    h = byte_step<MODE>(h, w & 0xffu, tab);
-    h = byte_step<MODE>(h, (w >> 8) & 0xffu, tab);
-    h = byte_step<MODE>(h, (w >> 16) & 0xffu, tab);
-    h = byte_step<MODE>(h, w >> 24, tab);
+    h = byte_step<MODE, VAR>(h, w & 0xffu, tab, k);
+    h = byte_step<MODE, VAR>(h, (w >> 8) & 0xffu, tab, k);
+    h = byte_step<MODE, VAR>(h, (w >> 16) & 0xffu, tab, k);
+    h = byte_step<MODE, VAR>(h, w >> 24, tab, k);
     return h;
 }
 
-template <int MODE, class Src>
+template <int MODE, int VAR, class Src>
 __device__ __forceinline__ uint32_t hash_bytes(const Src &src, typename Src::pos_t p, uint32_t len,
                                                const uint32_t *tab)
 {
+    ShiftK k{0u, 0u, 0u};
+    if constexpr ((VAR & 1) != 0) k = opaque_shifts();
     QStream<Src> st;
     st.init(src, p);
     uint32_t h = byte_init<MODE>();
     const uint32_t n8 = len >> 3;
+#pragma unroll 2
     for (uint32_t i = 0; i < n8; i++) {
         uint2 w = st.next8();
-        h = word_bytes<MODE>(h, w.x, tab);
-        h = word_bytes<MODE>(h, w.y, tab);
+        h = word_bytes<MODE, VAR>(h, w.x, tab, k);
+        h = word_bytes<MODE, VAR>(h, w.y, tab, k);
     }
     const uint32_t rem = len & 7u;
     if (rem) {
         uint2 w = st.next8();
         if (rem >= 4) {
-            h = word_bytes<MODE>(h, w.x, tab);
+            h = word_bytes<MODE, VAR>(h, w.x, tab, k);
             w.x = w.y;
         }
-        for (uint32_t k = 0; k < (rem & 3u); k++) {
-            h = byte_step<MODE>(h, (w.x >> (8u * k)) & 0xffu, tab);
+        for (uint32_t j = 0; j < (rem & 3u); j++) {
+            h = byte_step<MODE, VAR>(h, (w.x >> (8u * j)) & 0xffu, tab, k);
         }
     }
     return byte_final<MODE>(h);
@@ -315,7 +359,7 @@ __device__ __forceinline__ uint32_t hash_md5_dev(const Src &src, typename Src::p
     return s[0]; /* digest bytes 0..3 little-endian (nc_md5.c:317-320) */
 }
 
-template <int MODE, class Src>
+template <int MODE, int VAR, class Src>
 __device__ __forceinline__ uint32_t hash_key(const Src &src, typename Src::pos_t p, uint32_t len,
                                              const uint32_t *tab)
 {
@@ -323,7 +367,7 @@ __device__ __forceinline__ uint32_t hash_key(const Src &src, typename Src::pos_t
     else if constexpr (MODE == NC_GPUHASH_HSIEH) return hash_hsieh_dev(src, p, len);
     else if constexpr (MODE == NC_GPUHASH_MURMUR) return hash_murmur_dev(src, p, len);
     else if constexpr (MODE == NC_GPUHASH_JENKINS) return hash_jenkins_dev(src, p, len);
-    else return hash_bytes<MODE>(src, p, len, tab);
+    else return hash_bytes<MODE, VAR>(src, p, len, tab);
 }
 
 template <int MODE>
@@ -335,110 +379,278 @@ constexpr bool uses_crc_table()
 /* Length class used to group keys of similar cost into one wave. */
 __device__ __forceinline__ uint32_t len_bucket(uint32_t len)
 {
-    uint32_t b = (len + 3u) >> 2;
-    return b < (uint32_t)(kBuckets - 1) ? b : (uint32_t)(kBuckets - 1);
+    return len < (uint32_t)(kBuckets - 1) ? len : (uint32_t)(kBuckets - 2);
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+/* LDS-only workgroup barrier: waits for this wave's LDS traffic, not for its
+ * vector-memory (LDS-DMA) loads, so the next tile's slab stays in flight. */
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0) only (gfx9 encoding: vmcnt/expcnt fields saturated) */
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+/* vmcnt(0) + lgkmcnt(0) + barrier, through the builtin so the compiler's
+ * waitcnt pass knows every earlier load has completed (an inline-asm wait is
+ * opaque to it and it would add its own vmcnt(0) later, e.g. behind a store). */
+__device__ __forceinline__ void full_barrier()
+{
+    __builtin_amdgcn_s_waitcnt(0x0070); /* vmcnt(0) expcnt(7) lgkmcnt(0) */
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+/* This lane's key [s, e) of a tile, loaded one tile ahead of its use: only
+ * the LOW dwords of the u64 offsets, since every use is 32-bit (the length,
+ * and the start relative to a slab base < 4 GiB away). Loads are clamped so
+ * every lane issues them (a fixed per-wave instruction count). */
+struct TileOffs {
+    uint32_t s, e;
+};
+
+__device__ __forceinline__ TileOffs load_offs(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
+                                              uint32_t t)
+{
+    uint64_t k = tile * (uint64_t)kTile + t;
+    uint64_t k1 = k + 1;
+    if (k > nkeys) k = nkeys;
+    if (k1 > nkeys) k1 = nkeys;
+    const uint32_t *o32 = reinterpret_cast<const uint32_t *>(off); /* little-endian: low dword first */
+    TileOffs o;
+    o.s = o32[2 * k];
+    o.e = o32[2 * k1];
+    return o;
+}
+
+__device__ __forceinline__ uint32_t tile_count(uint64_t tile, uint64_t nkeys)
+{
+    const uint64_t left = nkeys - tile * (uint64_t)kTile;
+    return left < (uint64_t)kTile ? (uint32_t)left : (uint32_t)kTile;
+}
+
+/* Slab bounds {off[k0], off[k0 + cnt]} of a tile, DMA'd into a ring slot by
+ * lanes 0-3 of every wave (four dwords; identical values from every wave).
+ * LDS-DMA keeps them out of VGPRs and out of lgkmcnt: nothing in the hash
+ * loop ever waits for them. Exactly one VMEM instruction per wave. */
+__device__ __forceinline__ void issue_bounds(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
+                                             uint8_t *slot, uint32_t lane)
+{
+    const uint64_t k0 = tile * (uint64_t)kTile;
+    const uint64_t k = k0 + (lane >= 2u ? tile_count(tile, nkeys) : 0u);
+    if (lane < 4u) {
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)(reinterpret_cast<const uint32_t *>(off + k) + (lane & 1u)),
+                                         (lds_void_t *)slot, 4, 0, 0);
+    }
+}
+
+/* staged bytes = span rounded up to 16 + 2 look-ahead pieces (the reader
+ * touches up to 18 bytes past a key) */
+__device__ __forceinline__ bool fits_lds(uint64_t span) { return span + 48u <= (uint64_t)kSlabCap; }
+
+/* Issue the LDS-DMA copy of a slab: 16-byte pieces, one 1 KiB wave-instruction
+ * per 64 pieces, landing contiguously at buf (wave-uniform base + lane*16). */
+__device__ __forceinline__ void issue_slab(const uint8_t *keys_base, uint64_t S16, uint64_t span, uint8_t *buf,
+                                           uint32_t t)
+{
+    const uint32_t nch = (uint32_t)((span + 15u) >> 4) + 2u; /* +2 pieces: reader look-ahead */
+    const uint32_t wbase = t & ~63u;
+#pragma unroll
+    for (int i = 0; i < kStageIters; i++) {
+        const uint32_t c = t + (uint32_t)i * kBlock;
+        if (wbase + (uint32_t)i * kBlock < nch && c < nch) {
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)(keys_base + S16 + 16u * c),
+                                             (lds_void_t *)(buf + 16u * (wbase + (uint32_t)i * kBlock)), 16, 0, 0);
+        }
+    }
+}
+
+/* L2 prefetch of a tile PD tiles ahead (PD = 2..4): one dword per 64-byte
+ * sector, DMA'd into a dump area nobody reads. Lanes 0..223 touch the slab
+ * (14 KiB), lanes 224..255 the tile's 2 KiB of offsets. It moves that tile's
+ * HBM latency off the critical path without spending LDS or VGPRs on
+ * buffering: the real staging DMA and offset loads later hit L2. Exactly one
+ * VMEM instruction per wave; addresses clamped into the slab / offsets. */
+constexpr uint32_t kPfSlabLanes = 224;
+
+__device__ __forceinline__ void issue_prefetch(const uint8_t *keys_base, uint64_t S16, uint64_t span,
+                                               const uint64_t *off, uint64_t tile, uint64_t nkeys, uint8_t *dump,
+                                               uint32_t t)
+{
+    const uint8_t *p;
+    if (t < kPfSlabLanes) {
+        uint64_t o = 64u * (uint64_t)t;
+        if (o >= span) o = span > 4u ? ((span - 4u) & ~(uint64_t)3) : 0u;
+        p = keys_base + S16 + o;
+    } else {
+        uint64_t k = tile * (uint64_t)kTile + 8u * (t - kPfSlabLanes); /* 8 offsets per 64-byte sector */
+        if (k > nkeys) k = nkeys;
+        p = reinterpret_cast<const uint8_t *>(off + k);
+    }
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)p, (lds_void_t *)dump, 4, 0, 0);
+}
+
+__device__ __forceinline__ void read_bounds(const uint8_t *slot, uint64_t delta, uint64_t &S16, uint64_t &span)
+{
+    const uint64_t *b = reinterpret_cast<const uint64_t *>(slot);
+    const uint64_t S = b[0] + delta, E = b[1] + delta;
+    S16 = S & ~(uint64_t)15;
+    span = E - S16;
 }
 
 /*
- * keys_base is 16-byte aligned; key i occupies keys_base[off[i] + delta ..
- * off[i+1] + delta) and keys_base stays readable NC_GPUHASH_PAD bytes past
- * the last key.
+ * Persistent workgroups walk 256-key tiles grid-stride (tile t below means
+ * this workgroup's t-th tile). Iteration t:
+ *   top   : counted s_waitcnt + barrier — slab(t), offsets(t) and the bounds
+ *           ring are in; only the previous iteration's L2 prefetch (PF) may
+ *           still be in flight;
+ *   issue : store of tile t-1's hashes (late, so it drains under this tile),
+ *           bounds(t+3) -> ring, LDS-DMA of slab(t+1) into the other buffer,
+ *           offsets(t+1), L2 prefetch of slab(t+2) (PF);
+ *   work  : optional length sort, hash every key from LDS (or from global
+ *           memory when the slab exceeds the LDS budget).
+ * keys_base is 16-byte aligned; key i is keys_base[off[i]+delta, off[i+1]+delta)
+ * and keys_base stays readable NC_GPUHASH_PAD bytes past the last key.
  */
-template <int MODE, bool SORT>
+template <int MODE, bool SORT, int VAR>
 __global__ __launch_bounds__(kBlock) void nc_hash_kernel(const uint8_t *__restrict__ keys_base,
                                                          const uint64_t *__restrict__ off, uint64_t delta,
                                                          uint64_t nkeys, uint32_t *__restrict__ out,
                                                          uint64_t ntiles)
 {
+    /* VAR bits 1-2: L2-prefetch distance code (0 off, 1..3 -> 2..4 tiles ahead) */
+    constexpr uint32_t PD = ((VAR >> 1) & 3) ? (uint32_t)((VAR >> 1) & 3) + 1u : 0u;
+    constexpr bool PF = PD != 0;
+    /* bounds are DMA'd DB tiles ahead: slab issue needs t+1, prefetch t+PD,
+     * and both must be older than the previous iteration's prefetch */
+    constexpr uint32_t DB = PD + 1u > 3u ? PD + 1u : 3u;
+    static_assert(DB + 1u <= kRing, "bounds ring too small");
     __shared__ __attribute__((aligned(16))) uint8_t smem[kSmemBytes];
-    uint8_t *slab = smem + kOffSlab;
-    uint32_t *kstart = reinterpret_cast<uint32_t *>(smem + kOffStart);
-    uint32_t *klen = reinterpret_cast<uint32_t *>(smem + kOffLen);
+    uint32_t *kpos = reinterpret_cast<uint32_t *>(smem + kOffKey);
     uint16_t *perm = reinterpret_cast<uint16_t *>(smem + kOffPerm);
-    uint32_t *hist = reinterpret_cast<uint32_t *>(smem + kOffHist);
-    uint32_t *flag = reinterpret_cast<uint32_t *>(smem + kOffFlag);
+    uint32_t *hist2 = reinterpret_cast<uint32_t *>(smem + kOffHist); /* [2][kBuckets], by iteration parity */
+    uint32_t *flag2 = reinterpret_cast<uint32_t *>(smem + kOffFlag); /* [2] */
     uint32_t *tab = reinterpret_cast<uint32_t *>(smem + kOffTab);
+    uint8_t *ring = smem + kOffRing;
+    uint8_t *dump = smem + kOffDump;
 
     const uint32_t t = threadIdx.x;
     const uint32_t lane = t & 63u;
+    const uint64_t stride = gridDim.x;
+    uint64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    auto tile_at = [&](uint64_t j) -> uint64_t { /* j-th tile of this workgroup, clamped */
+        const uint64_t x = tile + j * stride;
+        return x < ntiles ? x : tile;
+    };
 
     if constexpr (uses_crc_table<MODE>()) {
         tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
-        __syncthreads();
+    }
+    if constexpr (SORT) {
+        if (t < 2u * kBuckets) hist2[t] = 0;
+        if (t < 2u) flag2[t] = 0;
     }
 
-    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    /* prologue: bounds of tiles 0..DB-1 into ring slots 0..DB-1 */
+#pragma unroll
+    for (uint32_t j = 0; j < DB; j++) issue_bounds(off, tile_at(j), nkeys, ring + j * 16, lane);
+    full_barrier();
+    uint64_t S16, span;
+    read_bounds(ring, delta, S16, span);
+    uint32_t cnt = tile_count(tile, nkeys);
+    if (fits_lds(span)) issue_slab(keys_base, S16, span, smem + kOffSlab0, t);
+    asm volatile("" ::: "memory");
+    TileOffs cur = load_offs(off, tile, nkeys, t);
+    if constexpr (PF) {
+#pragma unroll
+        for (uint32_t j = 1; j < PD; j++) {
+            uint64_t pS, pspan;
+            read_bounds(ring + j * 16, delta, pS, pspan);
+            issue_prefetch(keys_base, pS, pspan, off, tile_at(j), nkeys, dump, t);
+        }
+    }
+    uint64_t pend_idx = ~0ull;
+    uint32_t pend_h = 0;
+
+    /* one tile; `cur` holds its offsets, `nn` receives the next tile's */
+    auto step = [&](TileOffs &cur, TileOffs &nn, uint32_t it) __attribute__((always_inline)) {
+        uint8_t *slab = smem + ((it & 1u) ? kOffSlab1 : kOffSlab0);
+        uint8_t *slab_next = smem + ((it & 1u) ? kOffSlab0 : kOffSlab1);
+        const bool in_lds = fits_lds(span);
+        const uint64_t myS16 = S16;
+        const uint32_t mycnt = cnt;
         const uint64_t k0 = tile * (uint64_t)kTile;
-        const uint64_t left = nkeys - k0;
-        const uint32_t cnt = left < (uint64_t)kTile ? (uint32_t)left : (uint32_t)kTile;
-        const bool valid = t < cnt;
 
-        uint64_t s = 0, e = 0;
-        if (valid) {
-            s = off[k0 + t];
-            e = off[k0 + t + 1];
+        /* Everything but the youngest VMEM instruction of the previous
+         * iteration (its L2 prefetch) must have landed. */
+        if constexpr (PF) {
+            __builtin_amdgcn_s_waitcnt(0x0071); /* vmcnt(1) expcnt(7) lgkmcnt(0) */
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        } else {
+            full_barrier();
         }
-        const uint64_t S = off[k0] + delta;
-        const uint64_t E = off[k0 + cnt] + delta;
-        const uint64_t S16 = S & ~(uint64_t)15;
-        const uint64_t span = E - S16;
-        const bool in_lds = span + 16u <= (uint64_t)kSlabCap;
-        const uint32_t len = (uint32_t)(e - s);
+        if (pend_idx != ~0ull) out[pend_idx] = pend_h;
+        pend_idx = ~0ull;
+        asm volatile("" ::: "memory");
 
-        if (in_lds) {
-            /* coalesced 16-byte staging of [S16, roundup16(E) + 16) */
-            const uint32_t nch = (uint32_t)((span + 15u) >> 4) + 1u;
-            const uint4 *g = reinterpret_cast<const uint4 *>(keys_base + S16);
-            uint4 *l = reinterpret_cast<uint4 *>(slab);
-            uint4 v[kStageIters];
-#pragma unroll
-            for (int i = 0; i < kStageIters; i++) {
-                const uint32_t c = t + (uint32_t)i * kBlock;
-                if (c < nch) v[i] = g[c];
-            }
-#pragma unroll
-            for (int i = 0; i < kStageIters; i++) {
-                const uint32_t c = t + (uint32_t)i * kBlock;
-                if (c < nch) l[c] = v[i];
-            }
+        const uint64_t t1 = tile + stride;
+        issue_bounds(off, tile_at(DB), nkeys, ring + ((it + DB) % kRing) * 16, lane);
+        asm volatile("" ::: "memory");
+        if (t1 < ntiles) {
+            read_bounds(ring + ((it + 1u) % kRing) * 16, delta, S16, span);
+            cnt = tile_count(t1, nkeys);
+            if (fits_lds(span)) issue_slab(keys_base, S16, span, slab_next, t);
         }
+        asm volatile("" ::: "memory");
+        if constexpr ((VAR & 16) != 0) {
+            /* DIAGNOSTIC ONLY: C3's arithmetic layout (32-byte keys) instead of
+             * loading offsets -- isolates the cost of the offsets path */
+            const uint64_t kk = (t1 < ntiles ? t1 : tile) * (uint64_t)kTile + t;
+            nn.s = (uint32_t)(kk * 32u);
+            nn.e = (uint32_t)(kk * 32u + 32u);
+        } else {
+            nn = load_offs(off, t1 < ntiles ? t1 : tile, nkeys, t);
+        }
+        if constexpr (PF) {
+            asm volatile("" ::: "memory");
+            uint64_t pS, pspan;
+            read_bounds(ring + ((it + PD) % kRing) * 16, delta, pS, pspan);
+            issue_prefetch(keys_base, pS, pspan, off, tile_at(PD), nkeys, dump, t);
+        }
+
+        const bool valid = t < mycnt;
+        const uint32_t len = valid ? cur.e - cur.s : 0u;
+        const uint32_t rel = cur.s + (uint32_t)delta - (uint32_t)myS16;
 
         uint32_t my = t;
+        bool sorted = false;
         if constexpr (SORT) {
-            /* Group keys by length class: wave-ballot multisplit, one LDS
-             * atomic per (wave, class), then an exclusive scan over classes. */
+            /* Group the tile's keys by length so each wave hashes keys of one
+             * cost: skipped (one extra barrier) when no wave mixes lengths,
+             * and for tiles too long for LDS (start and length must fit 16 bits). */
+            uint32_t *hist = hist2 + (it & 1u) * kBuckets;
             const uint32_t bucket = valid ? len_bucket(len) : (uint32_t)(kBuckets - 1);
-            if (t < (uint32_t)kBuckets) hist[t] = 0;
-            if (t == 0) flag[0] = 0;
-            kstart[t] = in_lds ? (uint32_t)(s + delta - S16) : 0u;
-            klen[t] = len;
-            __syncthreads();
             const uint32_t b0 = __shfl(bucket, 0);
-            if (__ballot(bucket != b0) != 0ull && lane == 0) flag[0] = 1u;
-            /* flag only grows: any lane writing 1 makes the tile sortable */
-            __syncthreads();
-            if (flag[0] != 0u) {
-                const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
-                uint32_t rank = 0;
-                bool done = false;
-                while (true) {
-                    const uint64_t act = __ballot(!done);
-                    if (act == 0ull) break;
-                    const uint32_t lead = (uint32_t)__ffsll((unsigned long long)act) - 1u;
-                    const uint32_t bl = __shfl(bucket, (int)lead);
-                    const bool mine = !done && bucket == bl;
-                    const uint64_t m = __ballot(mine);
-                    uint32_t base = 0;
-                    if (lane == lead) base = atomicAdd(&hist[bl], (uint32_t)__popcll(m));
-                    base = __shfl(base, (int)lead);
-                    if (mine) {
-                        rank = base + (uint32_t)__popcll(m & lt);
-                        done = true;
-                    }
-                }
-                __syncthreads();
+            if (in_lds && __ballot(bucket != b0) != 0ull && lane == 0) flag2[it & 1u] = 1u;
+            /* the other parity's state was last read before this tile's top
+             * barrier: clear it for the next tile */
+            if (t < (uint32_t)kBuckets) hist2[((it + 1u) & 1u) * kBuckets + t] = 0;
+            if (t == 0) flag2[(it + 1u) & 1u] = 0;
+            lds_barrier();
+            if (flag2[it & 1u] != 0u) {
+                sorted = true;
+                kpos[t] = rel | (len << 16);
+                const uint32_t rank = atomicAdd(&hist[bucket], 1u);
+                lds_barrier();
                 if (t < 64u) {
-                    /* exclusive scan of the 64 class counts by wave 0 */
                     const uint32_t c = hist[t];
                     uint32_t x = c;
 #pragma unroll
@@ -448,40 +660,349 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel(const uint8_t *__restri
                     }
                     hist[t] = x - c;
                 }
-                __syncthreads();
+                lds_barrier();
                 perm[hist[bucket] + rank] = (uint16_t)t;
-                __syncthreads();
+                lds_barrier();
                 my = perm[t];
             }
         }
 
-        if (my < cnt) {
-            uint32_t h;
+        if (my < mycnt) {
             uint32_t klen_my = len;
-            if constexpr (SORT) klen_my = klen[my];
-            if (in_lds) {
-                uint32_t pos = (uint32_t)(s + delta - S16);
-                if constexpr (SORT) pos = kstart[my];
-                LdsSrc src{slab};
-                h = hash_key<MODE>(src, pos, klen_my, tab);
-            } else {
-                uint64_t pos = s + delta;
-                if constexpr (SORT) {
-                    if (my != t) pos = off[k0 + my] + delta;
-                }
-                GlobalSrc src{keys_base};
-                h = hash_key<MODE>(src, pos, klen_my, tab);
+            uint32_t pos = rel;
+            if (sorted) {
+                const uint32_t kp = kpos[my];
+                pos = kp & 0xffffu;
+                klen_my = kp >> 16;
             }
-            out[k0 + my] = h;
+            uint32_t h;
+            if constexpr ((VAR & 8) != 0) {
+                /* DIAGNOSTIC ONLY (never the default): staging, offsets and
+                 * stores as usual, no key reads and no hashing -- the
+                 * memory-pipeline ceiling of this kernel structure */
+                h = pos ^ klen_my;
+            } else if (in_lds) {
+                LdsSrc src{reinterpret_cast<const uint32_t *>(slab)};
+                h = hash_key<MODE, VAR>(src, pos, klen_my, tab);
+            } else {
+                GlobalSrc src{reinterpret_cast<const uint32_t *>(keys_base)};
+                h = hash_key<MODE, VAR>(src, myS16 + pos, klen_my, tab);
+                /* retire the reader's look-ahead load here, so no register
+                 * write is left pending where the two paths merge (the
+                 * compiler would otherwise wait vmcnt(0) after the merge,
+                 * i.e. on the L2 prefetch too) */
+                __builtin_amdgcn_s_waitcnt(0x0070);
+            }
+            pend_idx = k0 + my;
+            pend_h = h;
         }
-        __syncthreads(); /* the next tile restages the LDS */
+    };
+    /* Unrolled by two with the offset registers swapping roles, so a loaded
+     * register is never copied at the back-edge (a copy would make the
+     * compiler wait vmcnt(0) there — on the L2 prefetch as well). */
+    TileOffs other;
+    for (uint32_t it = 0;;) {
+        if (tile >= ntiles) break;
+        step(cur, other, it++);
+        tile += stride;
+        if (tile >= ntiles) break;
+        step(other, cur, it++);
+        tile += stride;
     }
+    if (pend_idx != ~0ull) out[pend_idx] = pend_h;
+}
+
+/* ---------------- register-staged pipeline (variant bit 5) ----------------
+ *
+ * Same tiles, same hashing, different staging: every lane keeps the NEXT-BUT-
+ * ONE tile's slab pieces in VGPRs (kRsK x 16 bytes, ordinary coalesced
+ * global_load_dwordx4 = 1 KiB per wave-instruction) while the next tile's
+ * pieces are still landing, and copies a tile into the single LDS slab
+ * buffer just before hashing it. Two slabs per workgroup are in flight
+ * without a second LDS buffer, so twice the bytes per CU are outstanding
+ * (Little's law: that is what this HBM-latency-bound loop needs). Every load
+ * targets VGPRs, so hipcc's own waitcnt pass orders everything; register sets
+ * alternate by tile parity (loop unrolled by two) so no loaded register is
+ * ever copied.
+ */
+/* A tile's slab bounds by ONE vector load per wave (lane 0: off[k0],
+ * lane 1: off[k0 + cnt]), read back with v_readlane. A scalar load would
+ * count in lgkmcnt and stall the hashing loop's first LDS wait. */
+__device__ __forceinline__ uint64_t load_bounds(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
+                                                uint32_t lane)
+{
+    const uint64_t k0 = tile * (uint64_t)kTile;
+    return off[k0 + (lane == 1u ? tile_count(tile, nkeys) : 0u)];
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+constexpr int kRsK = 3;                                      /* 16-byte pieces per lane per tile */
+constexpr uint32_t kRsCap = (uint32_t)kRsK * kBlock * 16u;    /* 12 KiB slab */
+constexpr uint32_t kRsOffKey = kRsCap;
+constexpr uint32_t kRsOffPerm = kRsOffKey + 4 * kTile;
+constexpr uint32_t kRsOffHist = kRsOffPerm + 2 * kTile;
+constexpr uint32_t kRsOffFlag = kRsOffHist + 8 * kBuckets;
+constexpr uint32_t kRsOffTab = kRsOffFlag + 16;
+constexpr uint32_t kRsSmem = kRsOffTab + 4 * 256;
+static_assert(kRsOffTab % 16 == 0, "LDS carve must stay 16-byte aligned");
+static_assert(kRsCap < 65536, "sorted key positions are packed in 16 bits");
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+/* Named members, not an array: an array member passed by reference through
+ * a lambda was left in scratch memory by hipcc. */
+struct RsSlab {
+    u32x4_t a, b, c;
+};
+static_assert(kRsK == 3, "RsSlab holds three pieces per lane");
+
+/* Per-lane sink for the output stores of lanes without a key, so that every
+ * wave issues exactly one store per tile (the hand counts below rely on it). */
+__device__ uint32_t g_rs_sink[kBlock];
+
+/* ---- hand-counted VMEM (inline asm: invisible to hipcc's waitcnt pass) ----
+ * Every load and store of the pipeline is issued here, unconditionally, so
+ * each wave issues exactly 7 VMEM instructions per tile in a fixed order:
+ *   O(j+1): 2 x global_load_dword      (this lane's key start / end, low dwords)
+ *   B(j+3): 1 x global_load_dwordx2    (slab bounds, lanes 0/1)
+ *   R(j+2): 3 x global_load_dwordx4    (slab pieces)
+ *   S(j)  : 1 x global_store_dword     (this lane's hash, or the sink)
+ * and waits with counted vmcnt(N) whose asm rewrites the guarded registers,
+ * so no use of a loaded value can be scheduled above its wait. */
+__device__ __forceinline__ uint32_t asm_ld32(const void *p)
+{
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ uint64_t asm_ld64(const void *p)
+{
+    u32x2_t v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return ((uint64_t)v.y << 32) | v.x;
+}
+__device__ __forceinline__ u32x4_t asm_ld128(const void *p)
+{
+    u32x4_t v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void asm_st32(void *p, uint32_t v)
+{
+    asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
+}
+
+/* Uniform per-tile staging facts, derived from the tile's bounds. */
+struct RsMeta {
+    uint64_t S16;   /* 16-byte aligned slab start (keys_base-relative) */
+    uint32_t nch;   /* 16-byte pieces covering the slab */
+    uint32_t cnt;   /* keys in the tile */
+    bool in_lds;    /* slab fits the LDS buffer */
+};
+
+__device__ __forceinline__ RsMeta rs_meta(uint64_t bnd, uint64_t tile, uint64_t nkeys, uint64_t delta)
+{
+    RsMeta m;
+    const uint64_t S = readlane64(bnd, 0) + delta;
+    const uint64_t E = readlane64(bnd, 1) + delta;
+    m.S16 = S & ~(uint64_t)15;
+    const uint64_t span = E - m.S16;
+    m.in_lds = span <= (uint64_t)kRsCap;
+    m.nch = m.in_lds ? (uint32_t)((span + 15u) >> 4) : 0u;
+    m.cnt = tile_count(tile, nkeys);
+    return m;
+}
+
+__device__ __forceinline__ RsSlab rs_load(const uint8_t *keys_base, const RsMeta &m, uint32_t t)
+{
+    const u32x4_t *g = reinterpret_cast<const u32x4_t *>(keys_base + m.S16);
+    const uint32_t last = m.nch ? m.nch - 1u : 0u;
+    const uint32_t c0 = t, c1 = t + kBlock, c2 = t + 2u * kBlock;
+    RsSlab r;
+    r.a = asm_ld128(g + (c0 < last ? c0 : last));
+    r.b = asm_ld128(g + (c1 < last ? c1 : last));
+    r.c = asm_ld128(g + (c2 < last ? c2 : last));
+    return r;
+}
+
+__device__ __forceinline__ void rs_store_lds(uint8_t *slab, const RsMeta &m, uint32_t t, const RsSlab &r)
+{
+    u32x4_t *l = reinterpret_cast<u32x4_t *>(slab);
+    if (t < m.nch) l[t] = r.a;
+    if (t + kBlock < m.nch) l[t + kBlock] = r.b;
+    if (t + 2u * kBlock < m.nch) l[t + 2u * kBlock] = r.c;
+}
+
+__device__ __forceinline__ TileOffs rs_offs(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
+                                            uint32_t t)
+{
+    uint64_t k = tile * (uint64_t)kTile + t;
+    uint64_t k1 = k + 1;
+    if (k > nkeys) k = nkeys;
+    if (k1 > nkeys) k1 = nkeys;
+    TileOffs o;
+    o.s = asm_ld32(off + k);  /* low dword (little-endian) */
+    o.e = asm_ld32(off + k1);
+    return o;
+}
+
+__device__ __forceinline__ uint64_t rs_bounds(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
+                                              uint32_t lane)
+{
+    const uint64_t k0 = tile * (uint64_t)kTile;
+    return asm_ld64(off + k0 + (lane == 1u ? tile_count(tile, nkeys) : 0u));
+}
+
+template <int MODE, bool SORT, int VAR>
+__global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__restrict__ keys_base,
+                                                            const uint64_t *__restrict__ off, uint64_t delta,
+                                                            uint64_t nkeys, uint32_t *__restrict__ out,
+                                                            uint64_t ntiles)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kRsSmem];
+    uint8_t *slab = smem;
+    uint32_t *kpos = reinterpret_cast<uint32_t *>(smem + kRsOffKey);
+    uint16_t *perm = reinterpret_cast<uint16_t *>(smem + kRsOffPerm);
+    uint32_t *hist2 = reinterpret_cast<uint32_t *>(smem + kRsOffHist);
+    uint32_t *flag2 = reinterpret_cast<uint32_t *>(smem + kRsOffFlag);
+    uint32_t *tab = reinterpret_cast<uint32_t *>(smem + kRsOffTab);
+
+    const uint32_t t = threadIdx.x;
+    const uint32_t lane = t & 63u;
+    const uint64_t stride = gridDim.x;
+    const uint64_t tile0 = blockIdx.x;
+    if (tile0 >= ntiles) return;
+    auto tile_at = [&](uint64_t j) -> uint64_t {
+        const uint64_t x = tile0 + j * stride;
+        return x < ntiles ? x : tile0;
+    };
+    uint32_t *sink = g_rs_sink + t;
+
+    if constexpr (uses_crc_table<MODE>()) {
+        tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
+    }
+    if constexpr (SORT) {
+        if (t < 2u * kBuckets) hist2[t] = 0;
+        if (t < 2u) flag2[t] = 0;
+    }
+
+    /* prologue: bounds of tiles 0 and 1 (waited), then the steady-state
+     * order as if steps -2 and -1 had run: R(0), S(-2), O(0), B(2), R(1), S(-1) */
+    uint64_t b0 = rs_bounds(off, tile_at(0), nkeys, lane);
+    uint64_t b1 = rs_bounds(off, tile_at(1), nkeys, lane);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(b0), "+v"(b1) : : "memory");
+    RsMeta m0 = rs_meta(b0, tile_at(0), nkeys, delta);
+    RsMeta m1 = rs_meta(b1, tile_at(1), nkeys, delta);
+    RsSlab ra = rs_load(keys_base, m0, t);
+    asm_st32(sink, 0u);
+    TileOffs oa = rs_offs(off, tile_at(0), nkeys, t);
+    TileOffs ob;
+    uint64_t bq = rs_bounds(off, tile_at(2), nkeys, lane);
+    RsSlab rb = rs_load(keys_base, m1, t);
+    asm_st32(sink, 0u);
+
+    /* tile j: slab in `r`, offsets in `oc`, next offsets into `on`; meta of
+     * tiles j, j+1 in mc / mn (mc receives tile j+2's at the end). */
+    auto step = [&](uint64_t j, RsSlab &r, TileOffs &oc, TileOffs &on, RsMeta &mc)
+        __attribute__((always_inline)) {
+        const uint64_t tile = tile0 + j * stride;
+        const uint64_t k0 = tile * (uint64_t)kTile;
+        lds_barrier(); /* everyone is done with the previous tile's LDS */
+        /* R(j): younger are S(j-2), O(j), B(j+2), R(j+1) x3, S(j-1) */
+        asm volatile("s_waitcnt vmcnt(8)" : "+v"(r.a), "+v"(r.b), "+v"(r.c) : : "memory");
+        if (mc.in_lds) rs_store_lds(slab, mc, t, r);
+        on = rs_offs(off, tile_at(j + 1), nkeys, t);
+        /* B(j+2): younger are R(j+1) x3, S(j-1), O(j+1) x2 */
+        asm volatile("s_waitcnt vmcnt(6)" : "+v"(bq) : : "memory");
+        const RsMeta m2 = rs_meta(bq, tile_at(j + 2), nkeys, delta);
+        bq = rs_bounds(off, tile_at(j + 3), nkeys, lane);
+        r = rs_load(keys_base, m2, t);
+        lds_barrier(); /* the slab is in LDS */
+        /* O(j): younger are B(j+2), R(j+1) x3, S(j-1), O(j+1) x2, B(j+3), R(j+2) x3 */
+        asm volatile("s_waitcnt vmcnt(11)" : "+v"(oc.s), "+v"(oc.e) : : "memory");
+
+        const bool valid = t < mc.cnt;
+        const uint32_t len = valid ? oc.e - oc.s : 0u;
+        const uint32_t rel = oc.s + (uint32_t)delta - (uint32_t)mc.S16;
+        uint32_t my = t;
+        bool sorted = false;
+        if constexpr (SORT) {
+            uint32_t *hist = hist2 + (uint32_t)(j & 1u) * kBuckets;
+            const uint32_t bucket = valid ? len_bucket(len) : (uint32_t)(kBuckets - 1);
+            const uint32_t bb = __shfl(bucket, 0);
+            if (mc.in_lds && __ballot(bucket != bb) != 0ull && lane == 0) flag2[j & 1u] = 1u;
+            if (t < (uint32_t)kBuckets) hist2[(uint32_t)((j + 1u) & 1u) * kBuckets + t] = 0;
+            if (t == 0) flag2[(j + 1u) & 1u] = 0;
+            lds_barrier();
+            if (flag2[j & 1u] != 0u) {
+                sorted = true;
+                kpos[t] = rel | (len << 16);
+                const uint32_t rank = atomicAdd(&hist[bucket], 1u);
+                lds_barrier();
+                if (t < 64u) {
+                    const uint32_t c = hist[t];
+                    uint32_t x = c;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t y = __shfl_up(x, d);
+                        if (lane >= (uint32_t)d) x += y;
+                    }
+                    hist[t] = x - c;
+                }
+                lds_barrier();
+                perm[hist[bucket] + rank] = (uint16_t)t;
+                lds_barrier();
+                my = perm[t];
+            }
+        }
+        uint32_t h = 0;
+        if (my < mc.cnt) {
+            uint32_t klen_my = len, pos = rel;
+            if (sorted) {
+                const uint32_t kp = kpos[my];
+                pos = kp & 0xffffu;
+                klen_my = kp >> 16;
+            }
+            if (mc.in_lds) {
+                LdsSrc src{reinterpret_cast<const uint32_t *>(slab)};
+                h = hash_key<MODE, VAR>(src, pos, klen_my, tab);
+            } else {
+                /* long-key path: hipcc's own loads; it waits vmcnt(0) for
+                 * them, which is only an over-wait for the hand counts */
+                GlobalSrc src{reinterpret_cast<const uint32_t *>(keys_base)};
+                h = hash_key<MODE, VAR>(src, mc.S16 + pos, klen_my, tab);
+                __builtin_amdgcn_s_waitcnt(0x0070);
+            }
+        }
+        asm_st32(my < mc.cnt ? (void *)(out + k0 + my) : (void *)sink, h);
+        mc = m2;
+    };
+
+    for (uint64_t j = 0;;) {
+        if (tile0 + j * stride >= ntiles) break;
+        step(j, ra, oa, ob, m0);
+        j++;
+        if (tile0 + j * stride >= ntiles) break;
+        step(j, rb, ob, oa, m1);
+        j++;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
 }
 
 /* ---------------- launch layer ---------------- */
 
-int g_grid_cap = -1; /* 0 = one workgroup per tile */
+int g_grid_cap = -1; /* 0 = persistent: every resident workgroup slot once */
 int g_sort = -1;     /* 1 on, 0 off */
+int g_variant = 0;   /* bit 0: shift-add FNV multiply; bits 1-2: L2 prefetch distance code
+                        (0 off, 1..3 -> 2..4 tiles ahead); bit 3: diagnostic no-hash build
+                        (fnv1a_64, unsorted; outputs are not hashes) */
 
 int grid_cap()
 {
@@ -497,28 +1018,97 @@ bool sort_enabled()
 {
     if (g_sort < 0) {
         const char *e = getenv("NC_GPUHASH_SORT");
-        g_sort = e ? (atoi(e) ? 1 : 0) : 1;
+        g_sort = e ? (atoi(e) ? 1 : 0) : 0;
     }
     return g_sort == 1;
 }
 
-template <int MODE>
-hipError_t launch_mode(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys,
-                       uint32_t *out, hipStream_t stream, bool sort)
+int g_num_cus[64];
+
+int num_cus()
 {
-    const uint64_t ntiles = (nkeys + kTile - 1) / kTile;
-    uint64_t grid = ntiles;
-    const int cap = grid_cap();
-    if (cap > 0 && grid > (uint64_t)cap) grid = (uint64_t)cap;
-    if (grid > 0x7fffffffull) grid = 0x7fffffffull;
-    if (sort) {
-        hipLaunchKernelGGL((nc_hash_kernel<MODE, true>), dim3((unsigned)grid), dim3(kBlock), 0, stream, base, off,
-                           delta, nkeys, out, ntiles);
-    } else {
-        hipLaunchKernelGGL((nc_hash_kernel<MODE, false>), dim3((unsigned)grid), dim3(kBlock), 0, stream, base,
-                           off, delta, nkeys, out, ntiles);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (g_num_cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        g_num_cus[dev] = n;
     }
+    return g_num_cus[dev];
+}
+
+template <int MODE, bool SORT, int VAR>
+hipError_t launch_kernel(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                         hipStream_t stream)
+{
+    /* persistent grid: every resident workgroup slot once (occupancy query
+     * cached per instantiation), unless a cap is set */
+    void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t);
+    if constexpr ((VAR & 32) != 0) kern = nc_hash_kernel_rs<MODE, SORT, VAR>;
+    else kern = nc_hash_kernel<MODE, SORT, VAR>;
+    static int per_cu = 0;
+    if (per_cu == 0) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, kBlock, 0) != hipSuccess || b <= 0) b = 4;
+        per_cu = b;
+    }
+    const uint64_t ntiles = (nkeys + kTile - 1) / kTile;
+    const int cap = grid_cap();
+    uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu;
+    if (grid > ntiles) grid = ntiles;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, stream, base, off, delta, nkeys, out, ntiles);
     return hipGetLastError();
+}
+
+constexpr bool has_mul_variant(int mode) { return mode == NC_GPUHASH_FNV1A_64 || mode == NC_GPUHASH_FNV1_64; }
+
+template <int MODE, bool SORT>
+hipError_t launch_sorted(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                         hipStream_t stream, int var)
+{
+    /* variant bit 0: shift-add FNV multiply (FNV-64 modes); bits 1-2: L2
+     * prefetch distance code; bit 3: no-hash diagnostic (fnv1a_64 unsorted) */
+    if constexpr (has_mul_variant(MODE)) {
+        switch (var & 7) {
+        case 1: return launch_kernel<MODE, SORT, 1>(base, off, delta, nkeys, out, stream);
+        case 3: return launch_kernel<MODE, SORT, 3>(base, off, delta, nkeys, out, stream);
+        case 5: return launch_kernel<MODE, SORT, 5>(base, off, delta, nkeys, out, stream);
+        case 7: return launch_kernel<MODE, SORT, 7>(base, off, delta, nkeys, out, stream);
+        default: break;
+        }
+    }
+    if constexpr (MODE == NC_GPUHASH_FNV1A_64 && !SORT) {
+        if (var & 8) {
+            switch (var & 6) {
+            case 2: return launch_kernel<MODE, SORT, 10>(base, off, delta, nkeys, out, stream);
+            case 4: return launch_kernel<MODE, SORT, 12>(base, off, delta, nkeys, out, stream);
+            case 6: return launch_kernel<MODE, SORT, 14>(base, off, delta, nkeys, out, stream);
+            default: return launch_kernel<MODE, SORT, 8>(base, off, delta, nkeys, out, stream);
+            }
+        }
+        if (var & 16) return (var & 8) ? launch_kernel<MODE, SORT, 24>(base, off, delta, nkeys, out, stream)
+                                       : launch_kernel<MODE, SORT, 16>(base, off, delta, nkeys, out, stream);
+    }
+    if (var & 32) {
+        if constexpr (has_mul_variant(MODE)) {
+            if (var & 1) return launch_kernel<MODE, SORT, 33>(base, off, delta, nkeys, out, stream);
+        }
+        return launch_kernel<MODE, SORT, 32>(base, off, delta, nkeys, out, stream);
+    }
+    switch (var & 6) {
+    case 2: return launch_kernel<MODE, SORT, 2>(base, off, delta, nkeys, out, stream);
+    case 4: return launch_kernel<MODE, SORT, 4>(base, off, delta, nkeys, out, stream);
+    case 6: return launch_kernel<MODE, SORT, 6>(base, off, delta, nkeys, out, stream);
+    default: return launch_kernel<MODE, SORT, 0>(base, off, delta, nkeys, out, stream);
+    }
+}
+
+template <int MODE>
+hipError_t launch_mode(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                       hipStream_t stream, bool sort, int var)
+{
+    return sort ? launch_sorted<MODE, true>(base, off, delta, nkeys, out, stream, var)
+                : launch_sorted<MODE, false>(base, off, delta, nkeys, out, stream, var);
 }
 
 hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
@@ -530,7 +1120,7 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
     const bool sort = sort_enabled();
     switch (mode) {
 #define NC_CASE(M) \
-    case M: return launch_mode<M>(base, d_off, delta, nkeys, d_out, stream, sort);
+    case M: return launch_mode<M>(base, d_off, delta, nkeys, d_out, stream, sort, g_variant);
         NC_CASE(NC_GPUHASH_ONE_AT_A_TIME)
         NC_CASE(NC_GPUHASH_MD5)
         NC_CASE(NC_GPUHASH_CRC16)
@@ -568,10 +1158,11 @@ extern "C" rstatus_t nc_gpuhash_batch_device(int mode, const uint8_t *d_keys, co
     return NC_OK;
 }
 
-extern "C" rstatus_t nc_gpuhash_set_tuning(int grid_cap_, int sort)
+extern "C" rstatus_t nc_gpuhash_set_tuning(int grid_cap_, int sort, int variant)
 {
     if (grid_cap_ >= 0) g_grid_cap = grid_cap_;
     if (sort >= 0) g_sort = sort ? 1 : 0;
+    if (variant >= 0) g_variant = variant;
     return NC_OK;
 }
 

@@ -1,0 +1,83 @@
+/* STREAM-style HBM read probe (include/nc_gpuhash_probe.h). */
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+
+#include "nc_gpuhash_probe.h"
+
+namespace {
+
+constexpr int kProbeBlock = 256;
+constexpr int kProbeUnroll = 8;
+
+/* Each workgroup streams contiguous 16-byte pieces, kProbeUnroll loads in
+ * flight per lane, and xors everything into one word so nothing is dead. */
+__global__ __launch_bounds__(kProbeBlock) void probe_read_kernel(const uint4 *__restrict__ p, uint64_t n16,
+                                                                 uint32_t *__restrict__ sink)
+{
+    uint32_t acc = 0;
+    const uint64_t step = (uint64_t)gridDim.x * kProbeBlock * kProbeUnroll;
+    for (uint64_t base = (uint64_t)blockIdx.x * kProbeBlock * kProbeUnroll + threadIdx.x; base < n16;
+         base += step) {
+        uint4 v[kProbeUnroll];
+#pragma unroll
+        for (int u = 0; u < kProbeUnroll; u++) {
+            const uint64_t i = base + (uint64_t)u * kProbeBlock;
+            v[u] = i < n16 ? p[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kProbeUnroll; u++) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    for (int d = 32; d > 0; d >>= 1) acc ^= __shfl_xor(acc, d);
+    if ((threadIdx.x & 63u) == 0) atomicXor(&sink[blockIdx.x], acc);
+}
+
+} // namespace
+
+extern "C" rstatus_t nc_gpuhash_probe_read(const void *d_buf, uint64_t bytes, uint32_t *d_sink, void *stream,
+                                           int iters, float *avg_ms)
+{
+    if (d_buf == nullptr || d_sink == nullptr || avg_ms == nullptr || iters <= 0 || (bytes & 15u)) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        errno = ENODEV;
+        return NC_ERROR;
+    }
+    unsigned grid = (unsigned)cus * 8u;
+    if (grid > 65536u) grid = 65536u;
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess) {
+        errno = ENODEV;
+        return NC_ERROR;
+    }
+    if (hipEventCreate(&b) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        errno = ENODEV;
+        return NC_ERROR;
+    }
+    hipLaunchKernelGGL(probe_read_kernel, dim3(grid), dim3(kProbeBlock), 0, st, (const uint4 *)d_buf, bytes / 16,
+                       d_sink);
+    (void)hipEventRecord(a, st);
+    for (int i = 0; i < iters; i++) {
+        hipLaunchKernelGGL(probe_read_kernel, dim3(grid), dim3(kProbeBlock), 0, st, (const uint4 *)d_buf,
+                           bytes / 16, d_sink);
+    }
+    (void)hipEventRecord(b, st);
+    rstatus_t rc = NC_OK;
+    float ms = 0.f;
+    if (hipGetLastError() != hipSuccess || hipEventSynchronize(b) != hipSuccess ||
+        hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+        errno = EIO;
+        rc = NC_ERROR;
+    } else {
+        *avg_ms = ms / (float)iters;
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return rc;
+}
