@@ -105,7 +105,9 @@ rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, const uint64_t
  * before hashing (1 on, 0 off, -1 keep). variant: kernel code variant bits
  * (bit 0: shift-add FNV-64 multiply; bits 1-2: L2 prefetch distance code,
  * 0 off, 1..3 = 2..4 tiles ahead; bit 3: DIAGNOSTIC no-hash build, fnv1a_64
- * unsorted only, outputs are NOT hashes; -1 = keep). */
+ * unsorted only, outputs are NOT hashes; bit 4: DIAGNOSTIC arithmetic offsets
+ * for fixed 32-byte keys, fnv1a_64 unsorted only; bit 5: register-staged
+ * pipeline, two tiles in flight; -1 = keep). */
 rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
 /* ---- 3b. host batches through a context (pinned staging, one stream per slot) ---- */

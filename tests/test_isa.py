@@ -1,0 +1,81 @@
+"""Static ISA checks of the gfx950 code object (CPU only; compiles to .s).
+
+The register-staged kernel issues its loads in inline asm and waits with
+hand-counted vmcnt(N). tools/check_vmcnt.py walks every feasible path of the
+kernel's basic-block graph, models the in-order counter, and fails if any
+instruction touches a VGPR whose inline-asm load is still in flight (the
+hazard behind a GPU fault seen during development: an unused load result
+whose register hipcc reassigned)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+ASM = os.path.join(ROOT, "twemproxy_amd", "csrc", "build", "nc_gpuhash_kernels.s")
+
+
+@pytest.fixture(scope="module")
+def asm_file():
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "twemproxy_amd", "csrc"), "asm"],
+                       capture_output=True, text=True)
+    if r.returncode != 0 or not os.path.exists(ASM):
+        pytest.fail("could not generate kernel assembly: " + r.stderr[-2000:])
+    return ASM
+
+
+def test_no_inflight_register_hazards(asm_file):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_vmcnt.py"), asm_file,
+                        "nc_hash_kernel_rs"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert "exploration bound" not in r.stdout
+
+
+BAD = """_Z3badv:
+\t;;#ASMSTART
+\tglobal_load_dwordx4 v[2:5], v[0:1], off
+\t;;#ASMEND
+\t;;#ASMSTART
+\tglobal_load_dword v6, v[0:1], off
+\t;;#ASMEND
+\ts_cbranch_execz .LBB0_2
+\t;;#ASMSTART
+\ts_waitcnt vmcnt(1)
+\t;;#ASMEND
+\tds_write_b128 v7, v[2:5]
+\ts_branch .LBB0_3
+.LBB0_2:
+\tds_write_b128 v7, v[2:5]
+.LBB0_3:
+\ts_endpgm
+"""
+
+
+def test_checker_flags_a_short_path(tmp_path):
+    """the wait sits on one branch only: the other path reads v[2:5] in flight"""
+    f = tmp_path / "bad.s"
+    f.write_text(BAD)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_vmcnt.py"), str(f)],
+                       capture_output=True, text=True)
+    assert r.returncode == 1 and "1 report(s)" in r.stdout, r.stdout
+
+
+def test_no_scratch_in_hash_kernels(asm_file):
+    text = open(asm_file).read()
+    for block in text.split(".amdhsa_kernel ")[1:]:
+        name = block.split()[0]
+        if "nc_hash_kernel" not in name:
+            continue
+        m = [l for l in block.splitlines() if ".amdhsa_private_segment_fixed_size" in l]
+        assert m and m[0].split()[-1] == "0", f"{name} uses scratch: {m}"
+
+
+def test_lds_fits_eight_workgroups(asm_file):
+    text = open(asm_file).read()
+    for block in text.split(".amdhsa_kernel ")[1:]:
+        name = block.split()[0]
+        if "nc_hash_kernel" not in name:
+            continue
+        lds = int([l for l in block.splitlines() if ".amdhsa_group_segment_fixed_size" in l][0].split()[-1])
+        assert lds * 8 <= 160 * 1024, (name, lds)

@@ -893,8 +893,8 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
         if (t < 2u) flag2[t] = 0;
     }
 
-    /* prologue: bounds of tiles 0 and 1 (waited), then the steady-state
-     * order as if steps -2 and -1 had run: R(0), S(-2), O(0), B(2), R(1), S(-1) */
+    /* Prologue: bounds of the first two tiles (waited), then the steady-state
+     * order as if steps -2 and -1 had run: R(0) S O(0) B(2) R(1) S */
     uint64_t b0 = rs_bounds(off, tile_at(0), nkeys, lane);
     uint64_t b1 = rs_bounds(off, tile_at(1), nkeys, lane);
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(b0), "+v"(b1) : : "memory");
@@ -902,30 +902,29 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
     RsMeta m1 = rs_meta(b1, tile_at(1), nkeys, delta);
     RsSlab ra = rs_load(keys_base, m0, t);
     asm_st32(sink, 0u);
-    TileOffs oa = rs_offs(off, tile_at(0), nkeys, t);
-    TileOffs ob;
+    TileOffs oa = rs_offs(off, tile_at(0), nkeys, t), ob;
     uint64_t bq = rs_bounds(off, tile_at(2), nkeys, lane);
     RsSlab rb = rs_load(keys_base, m1, t);
     asm_st32(sink, 0u);
 
-    /* tile j: slab in `r`, offsets in `oc`, next offsets into `on`; meta of
-     * tiles j, j+1 in mc / mn (mc receives tile j+2's at the end). */
+    /* tile j: slab in `r`, offsets in `oc`, next offsets into `on`, meta in
+     * `mc` (which receives tile j+D's meta at the end). */
     auto step = [&](uint64_t j, RsSlab &r, TileOffs &oc, TileOffs &on, RsMeta &mc)
         __attribute__((always_inline)) {
         const uint64_t tile = tile0 + j * stride;
         const uint64_t k0 = tile * (uint64_t)kTile;
         lds_barrier(); /* everyone is done with the previous tile's LDS */
-        /* R(j): younger are S(j-2), O(j), B(j+2), R(j+1) x3, S(j-1) */
+        /* R(j): younger are S(j-2) and the 7 ops of step j-1 */
         asm volatile("s_waitcnt vmcnt(8)" : "+v"(r.a), "+v"(r.b), "+v"(r.c) : : "memory");
         if (mc.in_lds) rs_store_lds(slab, mc, t, r);
         on = rs_offs(off, tile_at(j + 1), nkeys, t);
         /* B(j+2): younger are R(j+1) x3, S(j-1), O(j+1) x2 */
         asm volatile("s_waitcnt vmcnt(6)" : "+v"(bq) : : "memory");
-        const RsMeta m2 = rs_meta(bq, tile_at(j + 2), nkeys, delta);
-        bq = rs_bounds(off, tile_at(j + 3), nkeys, lane);
-        r = rs_load(keys_base, m2, t);
+        const RsMeta mD = rs_meta(bq, tile_at(j + 2u), nkeys, delta);
+        bq = rs_bounds(off, tile_at(j + 3u), nkeys, lane);
+        r = rs_load(keys_base, mD, t);
         lds_barrier(); /* the slab is in LDS */
-        /* O(j): younger are B(j+2), R(j+1) x3, S(j-1), O(j+1) x2, B(j+3), R(j+2) x3 */
+        /* O(j): younger are B, R x3, S of step j-1 and O x2, B, R x3 of step j */
         asm volatile("s_waitcnt vmcnt(11)" : "+v"(oc.s), "+v"(oc.e) : : "memory");
 
         const bool valid = t < mc.cnt;
@@ -982,7 +981,7 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
             }
         }
         asm_st32(my < mc.cnt ? (void *)(out + k0 + my) : (void *)sink, h);
-        mc = m2;
+        mc = mD;
     };
 
     for (uint64_t j = 0;;) {
