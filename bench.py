@@ -100,9 +100,16 @@ def sum_over_ranks(torch, x: float, dist_on: bool) -> float:
 
 
 def roofline(alg_bytes: float, kern_ms: float, traffic):
+    """achieved = algorithmic bytes per launch / measured launch time; traffic =
+    HBM bytes per launch from PMC counters (None when not measured)."""
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic["bytes_per_launch"] if traffic else None,
+         "alg_bytes_per_launch": int(alg_bytes)}
+    if traffic:
+        r["traffic_source"] = traffic["source"]
+        r["traffic_over_alg"] = round(traffic["bytes_per_launch"] / alg_bytes, 4)
+    return r
 
 
 def load_traffic(kernel_mode: str, workload: str):

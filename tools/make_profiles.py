@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Turn one tools/gpu_profile_round.sh output directory into the committed
+profiles/ artifacts of a round:
+
+  profiles/<round>_bench_kernel_stats.csv   rocprofv3 --kernel-trace --stats of `python3 bench.py`
+  profiles/<round>_bench_phases.json        per-phase kernel averages from the same trace, next
+                                            to bench.py's own HIP-event kernel time
+  profiles/<round>_bench.json               the bench line of the plain run (and the one under rocprof)
+  profiles/pmc_<round>.json                 FETCH_SIZE / WRITE_SIZE per launch -> HBM bytes
+                                            (gfx950 correction: read = 2 x FETCH_SIZE KB; MI355X_MICROARCH.md)
+  profiles/<round>_e2e.jsonl                end-to-end host batch benchmark (tools/nc_e2e_bench)
+
+    python tools/make_profiles.py gpurun_out/r01r r01
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(HERE, "tools"))
+from pmc_summary import counters  # noqa: E402
+
+# bench.py's launch order on one GPU: (label, warmup, timed) -- see bench.py main()
+BENCH_PHASES = [("C2 fnv1a_64", 3, 20), ("C2 md5", 1, 5), ("C3 fnv1a_64", 3, 20)]
+
+
+def hash_phases(trace_csv):
+    """consecutive runs of nc_hash_kernel dispatches, split where another kernel runs"""
+    rows = list(csv.DictReader(open(trace_csv)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    runs, cur = [], None
+    for r in rows:
+        name = r["Kernel_Name"]
+        if "nc_hash_kernel" in name:
+            short = name.replace("void (anonymous namespace)::", "").split("(")[0]
+            if cur is None or cur["kernel"] != short:
+                cur = {"kernel": short, "ns": []}
+                runs.append(cur)
+            cur["ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        else:
+            cur = None
+    return runs
+
+
+def main():
+    src, rnd = sys.argv[1], sys.argv[2]
+    dst = os.path.join(HERE, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    prof = os.path.join(src, "prof")
+    shutil.copy(os.path.join(prof, "bench_kernel_stats.csv"), os.path.join(dst, f"{rnd}_bench_kernel_stats.csv"))
+
+    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    under = json.loads(open(os.path.join(src, "bench_under_rocprof.json")).read().strip().splitlines()[-1])
+    runs = hash_phases(os.path.join(prof, "bench_kernel_trace.csv"))
+    if len(runs) != len(BENCH_PHASES):
+        raise SystemExit(f"expected {len(BENCH_PHASES)} hash-kernel phases, found {len(runs)}")
+    event_ms = {"C2 fnv1a_64": under["kernel_ms_rank0"], "C3 fnv1a_64": under["c3_fnv1a_64"]["kernel_ms"]}
+    phases = []
+    for (label, warm, timed), run in zip(BENCH_PHASES, runs):
+        ns = run["ns"]
+        assert len(ns) == warm + timed, (label, len(ns))
+        t = ns[warm:]
+        ph = {"phase": label, "kernel": run["kernel"], "dispatches": len(ns), "timed": len(t),
+              "avg_ms_timed": round(sum(t) / len(t) / 1e6, 4), "min_ms": round(min(t) / 1e6, 4),
+              "max_ms": round(max(t) / 1e6, 4)}
+        if label in event_ms:
+            ph["bench_hip_event_ms"] = event_ms[label]
+            ph["rel_diff"] = round(ph["avg_ms_timed"] / event_ms[label] - 1.0, 4)
+        phases.append(ph)
+    json.dump({"command": "rocprofv3 --kernel-trace --stats -- python3 bench.py", "phases": phases},
+              open(os.path.join(dst, f"{rnd}_bench_phases.json"), "w"), indent=1)
+    json.dump({"plain_run": bench, "under_rocprof": under}, open(os.path.join(dst, f"{rnd}_bench.json"), "w"),
+              indent=1)
+
+    pmc = {"note": "per launch of the hash kernel; hbm_read = 2 x FETCH_SIZE x 1024 (gfx950 reports half "
+                   "of a 16-B/lane stream, MI355X_MICROARCH.md HBM section), hbm_write = WRITE_SIZE x 1024; "
+                   "one counter per rocprofv3 pass; inputs as bench.py (tools/pmc_run.py, variant 0:0:0)",
+           "workloads": {}}
+    for cfg in ("C2", "C3"):
+        for mode in ("fnv1a_64", "md5"):
+            rec = {}
+            for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+                d = os.path.join(src, f"pmc_{cfg}_{mode}_{ctr}", "pmc_counter_collection.csv")
+                if not os.path.exists(d):
+                    continue
+                for k, v in counters(d).items():
+                    if k.startswith("nc_hash_kernel"):
+                        rec["kernel"] = k
+                        rec[ctr + "_KB"] = v[ctr]
+                        rec["dispatches"] = v["_dispatches"]
+            if "FETCH_SIZE_KB" in rec and "WRITE_SIZE_KB" in rec:
+                rd = 2.0 * rec["FETCH_SIZE_KB"] * 1024.0
+                wr = rec["WRITE_SIZE_KB"] * 1024.0
+                rec.update(hbm_read_bytes=round(rd), hbm_write_bytes=round(wr), hbm_bytes_per_launch=round(rd + wr))
+                pmc["workloads"].setdefault(cfg, {})[mode] = rec
+    json.dump(pmc, open(os.path.join(dst, f"pmc_{rnd}.json"), "w"), indent=1)
+    e2e = os.path.join(src, "e2e.jsonl")
+    if os.path.exists(e2e):
+        shutil.copy(e2e, os.path.join(dst, f"{rnd}_e2e.jsonl"))
+    print(json.dumps(phases, indent=1))
+    print(json.dumps(pmc["workloads"], indent=1))
+
+
+if __name__ == "__main__":
+    main()
