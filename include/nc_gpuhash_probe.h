@@ -20,6 +20,10 @@ extern "C" {
  * 4 * 65536 bytes. */
 rstatus_t nc_gpuhash_probe_read(const void *d_buf, uint64_t bytes, uint32_t *d_sink, void *stream, int iters,
                                 float *avg_ms);
+/* The same with non-temporal (nt) loads: the ceiling for a read-once stream
+ * under the cache policy of launch variant bit 6. */
+rstatus_t nc_gpuhash_probe_read_nt(const void *d_buf, uint64_t bytes, uint32_t *d_sink, void *stream, int iters,
+                                   float *avg_ms);
 
 #ifdef __cplusplus
 }

@@ -37,10 +37,12 @@ def gpu_hash(mode, keys_d, off_d):
 
 
 @pytest.fixture(params=[(0, 1, 0), (0, 0, 0), (37, 1, 1), (0, 0, 3), (5, 1, 2), (0, 0, 4), (3, 1, 6),
-                        (0, 0, 32), (0, 1, 32), (11, 1, 33), (9, 0, 32)],
+                        (0, 0, 32), (0, 1, 32), (11, 1, 33), (9, 0, 32), (0, 0, 64), (0, 1, 64),
+                        (0, 0, 96), (7, 1, 96)],
                 ids=["persistent+sort", "persistent", "grid37+sort+shiftadd", "shiftadd+pf2",
                      "grid5+sort+pf2", "pf3", "grid3+sort+pf4", "regstage", "regstage+sort",
-                     "grid11+regstage+sort+shiftadd", "grid9+regstage"])
+                     "grid11+regstage+sort+shiftadd", "grid9+regstage", "nt", "nt+sort", "regstage+nt",
+                     "grid7+regstage+nt+sort"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)
@@ -193,7 +195,7 @@ def test_sort_and_grid_variants_agree_full_size(gpu):
     ref = None
     for grid, sort, var in ((0, 1, 0), (0, 0, 0), (2048, 1, 1), (4096, 0, 1), (1, 0, 0), (0, 0, 2), (0, 1, 2),
                             (3, 1, 3), (0, 0, 4), (7, 0, 6), (0, 0, 32), (0, 1, 32), (5, 1, 33), (13, 1, 32), (1024, 0, 32),
-                            (1536, 0, 32), (2048, 1, 32)):
+                            (1536, 0, 32), (2048, 1, 32), (0, 0, 64), (0, 1, 64), (0, 0, 96), (1536, 1, 96)):
         L.lib().nc_gpuhash_set_tuning(grid, sort, var)
         out = t.hash_batch_device("fnv1a_64", kd, od)
         torch.cuda.synchronize()

@@ -11,6 +11,8 @@ profiles/ artifacts of a round:
   profiles/<round>_e2e.jsonl                end-to-end host batch benchmark (tools/nc_e2e_bench)
 
     python tools/make_profiles.py gpurun_out/r01r r01
+    python tools/make_profiles.py --modes gpurun_out/r01s r01   (tools/gpu_modes.sh output ->
+                                                                 profiles/<round>_modes_c3.json)
 """
 import csv
 import json
@@ -44,7 +46,54 @@ def hash_phases(trace_csv):
     return runs
 
 
+MODE_NAMES = ["one_at_a_time", "md5", "crc16", "crc32", "crc32a", "fnv1_64", "fnv1a_64", "fnv1_32", "fnv1a_32",
+              "hsieh", "murmur", "jenkins"]
+
+
+def modes(src, rnd):
+    """all 12 modes on C3: in-process sweep (3 variants), kernel-trace stats and PMC bytes per launch"""
+    import re
+
+    dst = os.path.join(HERE, "profiles")
+    rows = [json.loads(l) for l in open(os.path.join(src, "sweep.log")) if l.startswith("{")]
+    probe = [r for r in rows if "probe_read_gbs" in r]
+    alg = 2 ** 31 + 12 * 2 ** 26
+    res = {"workload": "C3: 2^26 x 32 B keys, bytes 0x00-0xFF (seed 3)", "alg_bytes_per_launch": alg,
+           "hbm_peak_gbs": 8000.0, "probe_read_gbs": probe[0]["probe_read_gbs"] if probe else None,
+           "modes": {}}
+    for r in rows:
+        if "mode" not in r:
+            continue
+        key = f"grid{r['grid_cap']}_sort{r['sort']}_var{r['var']}"
+        m = res["modes"].setdefault(r["mode"], {"sweep_ms_median": {}})
+        m["sweep_ms_median"][key] = r["ms_median"]
+    stats = os.path.join(src, "trace", "modes_kernel_stats.csv")
+    for r in csv.DictReader(open(stats)):
+        mm = re.search(r"nc_hash_kernel<(\d+), (true|false), (\d+)>", r["Name"])
+        if mm:
+            name = MODE_NAMES[int(mm.group(1))]
+            res["modes"][name]["trace_avg_ms_var0"] = round(float(r["AverageNs"]) / 1e6, 4)
+            res["modes"][name]["trace_calls"] = int(r["Calls"])
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        for k, v in counters(os.path.join(src, f"pmc_{ctr}", "pmc_counter_collection.csv")).items():
+            mm = re.search(r"mode=(\d+)", k)
+            if mm:
+                res["modes"][MODE_NAMES[int(mm.group(1))]][ctr + "_KB"] = v[ctr]
+    for name, m in res["modes"].items():
+        v0 = m["sweep_ms_median"].get("grid0_sort0_var0")
+        if v0:
+            m["alg_gbs_var0"] = round(alg / (v0 * 1e-3) / 1e9, 1)
+            m["frac_var0"] = round(m["alg_gbs_var0"] / 8000.0, 4)
+        if "FETCH_SIZE_KB" in m and "WRITE_SIZE_KB" in m:
+            m["hbm_bytes_per_launch"] = round(2.0 * m["FETCH_SIZE_KB"] * 1024 + m["WRITE_SIZE_KB"] * 1024)
+            m["traffic_over_alg"] = round(m["hbm_bytes_per_launch"] / alg, 4)
+    json.dump(res, open(os.path.join(dst, f"{rnd}_modes_c3.json"), "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
 def main():
+    if sys.argv[1] == "--modes":
+        return modes(sys.argv[2], sys.argv[3])
     src, rnd = sys.argv[1], sys.argv[2]
     dst = os.path.join(HERE, "profiles")
     os.makedirs(dst, exist_ok=True)

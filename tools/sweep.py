@@ -41,7 +41,9 @@ def main():
         kb = int(off[-1].item())
         out = torch.empty(n, dtype=torch.int32, device="cuda")
         rd = [t.probe_read_gbs(keys, args.iters) for _ in range(args.rounds)]
+        rdn = [t.probe_read_gbs(keys, args.iters, nt=True) for _ in range(args.rounds)]
         print(json.dumps({"config": cfg, "probe_read_gbs": round(statistics.median(rd), 1),
+                          "probe_read_nt_gbs": round(statistics.median(rdn), 1),
                           "bytes": int(keys.numel())}), flush=True)
         modes = t.HASH_NAMES if args.modes == "all" else args.modes.split(",")
         for mode in modes:

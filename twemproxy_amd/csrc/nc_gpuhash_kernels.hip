@@ -414,6 +414,7 @@ struct TileOffs {
     uint32_t s, e;
 };
 
+template <bool NT = false>
 __device__ __forceinline__ TileOffs load_offs(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
                                               uint32_t t)
 {
@@ -423,8 +424,13 @@ __device__ __forceinline__ TileOffs load_offs(const uint64_t *__restrict__ off, 
     if (k1 > nkeys) k1 = nkeys;
     const uint32_t *o32 = reinterpret_cast<const uint32_t *>(off); /* little-endian: low dword first */
     TileOffs o;
-    o.s = o32[2 * k];
-    o.e = o32[2 * k1];
+    if constexpr (NT) { /* read-once stream: non-temporal */
+        o.s = __builtin_nontemporal_load(o32 + 2 * k);
+        o.e = __builtin_nontemporal_load(o32 + 2 * k1);
+    } else {
+        o.s = o32[2 * k];
+        o.e = o32[2 * k1];
+    }
     return o;
 }
 
@@ -438,6 +444,7 @@ __device__ __forceinline__ uint32_t tile_count(uint64_t tile, uint64_t nkeys)
  * lanes 0-3 of every wave (four dwords; identical values from every wave).
  * LDS-DMA keeps them out of VGPRs and out of lgkmcnt: nothing in the hash
  * loop ever waits for them. Exactly one VMEM instruction per wave. */
+template <int AUX = 0>
 __device__ __forceinline__ void issue_bounds(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
                                              uint8_t *slot, uint32_t lane)
 {
@@ -445,7 +452,7 @@ __device__ __forceinline__ void issue_bounds(const uint64_t *__restrict__ off, u
     const uint64_t k = k0 + (lane >= 2u ? tile_count(tile, nkeys) : 0u);
     if (lane < 4u) {
         __builtin_amdgcn_global_load_lds((gbl_void_t *)(reinterpret_cast<const uint32_t *>(off + k) + (lane & 1u)),
-                                         (lds_void_t *)slot, 4, 0, 0);
+                                         (lds_void_t *)slot, 4, 0, AUX);
     }
 }
 
@@ -455,6 +462,8 @@ __device__ __forceinline__ bool fits_lds(uint64_t span) { return span + 48u <= (
 
 /* Issue the LDS-DMA copy of a slab: 16-byte pieces, one 1 KiB wave-instruction
  * per 64 pieces, landing contiguously at buf (wave-uniform base + lane*16). */
+/* AUX: cache-policy bits of the DMA (2 = nt, for the read-once key stream) */
+template <int AUX = 0>
 __device__ __forceinline__ void issue_slab(const uint8_t *keys_base, uint64_t S16, uint64_t span, uint8_t *buf,
                                            uint32_t t)
 {
@@ -465,7 +474,7 @@ __device__ __forceinline__ void issue_slab(const uint8_t *keys_base, uint64_t S1
         const uint32_t c = t + (uint32_t)i * kBlock;
         if (wbase + (uint32_t)i * kBlock < nch && c < nch) {
             __builtin_amdgcn_global_load_lds((gbl_void_t *)(keys_base + S16 + 16u * c),
-                                             (lds_void_t *)(buf + 16u * (wbase + (uint32_t)i * kBlock)), 16, 0, 0);
+                                             (lds_void_t *)(buf + 16u * (wbase + (uint32_t)i * kBlock)), 16, 0, AUX);
         }
     }
 }
@@ -526,6 +535,8 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel(const uint8_t *__restri
     /* VAR bits 1-2: L2-prefetch distance code (0 off, 1..3 -> 2..4 tiles ahead) */
     constexpr uint32_t PD = ((VAR >> 1) & 3) ? (uint32_t)((VAR >> 1) & 3) + 1u : 0u;
     constexpr bool PF = PD != 0;
+    constexpr bool kNT = (VAR & 64) != 0;      /* variant bit 6: non-temporal key/offset/out streams */
+    constexpr int kAux = kNT ? 2 : 0;          /* global_load_lds cache-policy bits: 2 = nt */
     /* bounds are DMA'd DB tiles ahead: slab issue needs t+1, prefetch t+PD,
      * and both must be older than the previous iteration's prefetch */
     constexpr uint32_t DB = PD + 1u > 3u ? PD + 1u : 3u;
@@ -559,14 +570,14 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel(const uint8_t *__restri
 
     /* prologue: bounds of tiles 0..DB-1 into ring slots 0..DB-1 */
 #pragma unroll
-    for (uint32_t j = 0; j < DB; j++) issue_bounds(off, tile_at(j), nkeys, ring + j * 16, lane);
+    for (uint32_t j = 0; j < DB; j++) issue_bounds<kAux>(off, tile_at(j), nkeys, ring + j * 16, lane);
     full_barrier();
     uint64_t S16, span;
     read_bounds(ring, delta, S16, span);
     uint32_t cnt = tile_count(tile, nkeys);
-    if (fits_lds(span)) issue_slab(keys_base, S16, span, smem + kOffSlab0, t);
+    if (fits_lds(span)) issue_slab<kAux>(keys_base, S16, span, smem + kOffSlab0, t);
     asm volatile("" ::: "memory");
-    TileOffs cur = load_offs(off, tile, nkeys, t);
+    TileOffs cur = load_offs<kNT>(off, tile, nkeys, t);
     if constexpr (PF) {
 #pragma unroll
         for (uint32_t j = 1; j < PD; j++) {
@@ -597,17 +608,20 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel(const uint8_t *__restri
         } else {
             full_barrier();
         }
-        if (pend_idx != ~0ull) out[pend_idx] = pend_h;
+        if (pend_idx != ~0ull) {
+            if constexpr (kNT) __builtin_nontemporal_store(pend_h, out + pend_idx);
+            else out[pend_idx] = pend_h;
+        }
         pend_idx = ~0ull;
         asm volatile("" ::: "memory");
 
         const uint64_t t1 = tile + stride;
-        issue_bounds(off, tile_at(DB), nkeys, ring + ((it + DB) % kRing) * 16, lane);
+        issue_bounds<kAux>(off, tile_at(DB), nkeys, ring + ((it + DB) % kRing) * 16, lane);
         asm volatile("" ::: "memory");
         if (t1 < ntiles) {
             read_bounds(ring + ((it + 1u) % kRing) * 16, delta, S16, span);
             cnt = tile_count(t1, nkeys);
-            if (fits_lds(span)) issue_slab(keys_base, S16, span, slab_next, t);
+            if (fits_lds(span)) issue_slab<kAux>(keys_base, S16, span, slab_next, t);
         }
         asm volatile("" ::: "memory");
         if constexpr ((VAR & 16) != 0) {
@@ -617,7 +631,7 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel(const uint8_t *__restri
             nn.s = (uint32_t)(kk * 32u);
             nn.e = (uint32_t)(kk * 32u + 32u);
         } else {
-            nn = load_offs(off, t1 < ntiles ? t1 : tile, nkeys, t);
+            nn = load_offs<kNT>(off, t1 < ntiles ? t1 : tile, nkeys, t);
         }
         if constexpr (PF) {
             asm volatile("" ::: "memory");
@@ -776,10 +790,12 @@ __device__ uint32_t g_rs_sink[kBlock];
  *   S(j)  : 1 x global_store_dword     (this lane's hash, or the sink)
  * and waits with counted vmcnt(N) whose asm rewrites the guarded registers,
  * so no use of a loaded value can be scheduled above its wait. */
+template <bool NT = false>
 __device__ __forceinline__ uint32_t asm_ld32(const void *p)
 {
     uint32_t v;
-    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    if constexpr (NT) asm volatile("global_load_dword %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+    else asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
     return v;
 }
 __device__ __forceinline__ uint64_t asm_ld64(const void *p)
@@ -788,15 +804,19 @@ __device__ __forceinline__ uint64_t asm_ld64(const void *p)
     asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
     return ((uint64_t)v.y << 32) | v.x;
 }
+template <bool NT = false>
 __device__ __forceinline__ u32x4_t asm_ld128(const void *p)
 {
     u32x4_t v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    if constexpr (NT) asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+    else asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
     return v;
 }
+template <bool NT = false>
 __device__ __forceinline__ void asm_st32(void *p, uint32_t v)
 {
-    asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
+    if constexpr (NT) asm volatile("global_store_dword %0, %1, off nt" : : "v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
 }
 
 /* Uniform per-tile staging facts, derived from the tile's bounds. */
@@ -820,15 +840,16 @@ __device__ __forceinline__ RsMeta rs_meta(uint64_t bnd, uint64_t tile, uint64_t 
     return m;
 }
 
+template <bool NT>
 __device__ __forceinline__ RsSlab rs_load(const uint8_t *keys_base, const RsMeta &m, uint32_t t)
 {
     const u32x4_t *g = reinterpret_cast<const u32x4_t *>(keys_base + m.S16);
     const uint32_t last = m.nch ? m.nch - 1u : 0u;
     const uint32_t c0 = t, c1 = t + kBlock, c2 = t + 2u * kBlock;
     RsSlab r;
-    r.a = asm_ld128(g + (c0 < last ? c0 : last));
-    r.b = asm_ld128(g + (c1 < last ? c1 : last));
-    r.c = asm_ld128(g + (c2 < last ? c2 : last));
+    r.a = asm_ld128<NT>(g + (c0 < last ? c0 : last));
+    r.b = asm_ld128<NT>(g + (c1 < last ? c1 : last));
+    r.c = asm_ld128<NT>(g + (c2 < last ? c2 : last));
     return r;
 }
 
@@ -840,6 +861,7 @@ __device__ __forceinline__ void rs_store_lds(uint8_t *slab, const RsMeta &m, uin
     if (t + 2u * kBlock < m.nch) l[t + 2u * kBlock] = r.c;
 }
 
+template <bool NT>
 __device__ __forceinline__ TileOffs rs_offs(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
                                             uint32_t t)
 {
@@ -848,8 +870,8 @@ __device__ __forceinline__ TileOffs rs_offs(const uint64_t *__restrict__ off, ui
     if (k > nkeys) k = nkeys;
     if (k1 > nkeys) k1 = nkeys;
     TileOffs o;
-    o.s = asm_ld32(off + k);  /* low dword (little-endian) */
-    o.e = asm_ld32(off + k1);
+    o.s = asm_ld32<NT>(off + k);  /* low dword (little-endian) */
+    o.e = asm_ld32<NT>(off + k1);
     return o;
 }
 
@@ -884,6 +906,7 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
         return x < ntiles ? x : tile0;
     };
     uint32_t *sink = g_rs_sink + t;
+    constexpr bool kNT = (VAR & 64) != 0; /* variant bit 6: non-temporal streams */
 
     if constexpr (uses_crc_table<MODE>()) {
         tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
@@ -900,11 +923,11 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(b0), "+v"(b1) : : "memory");
     RsMeta m0 = rs_meta(b0, tile_at(0), nkeys, delta);
     RsMeta m1 = rs_meta(b1, tile_at(1), nkeys, delta);
-    RsSlab ra = rs_load(keys_base, m0, t);
+    RsSlab ra = rs_load<kNT>(keys_base, m0, t);
     asm_st32(sink, 0u);
-    TileOffs oa = rs_offs(off, tile_at(0), nkeys, t), ob;
+    TileOffs oa = rs_offs<kNT>(off, tile_at(0), nkeys, t), ob;
     uint64_t bq = rs_bounds(off, tile_at(2), nkeys, lane);
-    RsSlab rb = rs_load(keys_base, m1, t);
+    RsSlab rb = rs_load<kNT>(keys_base, m1, t);
     asm_st32(sink, 0u);
 
     /* tile j: slab in `r`, offsets in `oc`, next offsets into `on`, meta in
@@ -917,12 +940,12 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
         /* R(j): younger are S(j-2) and the 7 ops of step j-1 */
         asm volatile("s_waitcnt vmcnt(8)" : "+v"(r.a), "+v"(r.b), "+v"(r.c) : : "memory");
         if (mc.in_lds) rs_store_lds(slab, mc, t, r);
-        on = rs_offs(off, tile_at(j + 1), nkeys, t);
+        on = rs_offs<kNT>(off, tile_at(j + 1), nkeys, t);
         /* B(j+2): younger are R(j+1) x3, S(j-1), O(j+1) x2 */
         asm volatile("s_waitcnt vmcnt(6)" : "+v"(bq) : : "memory");
         const RsMeta mD = rs_meta(bq, tile_at(j + 2u), nkeys, delta);
         bq = rs_bounds(off, tile_at(j + 3u), nkeys, lane);
-        r = rs_load(keys_base, mD, t);
+        r = rs_load<kNT>(keys_base, mD, t);
         lds_barrier(); /* the slab is in LDS */
         /* O(j): younger are B, R x3, S of step j-1 and O x2, B, R x3 of step j */
         asm volatile("s_waitcnt vmcnt(11)" : "+v"(oc.s), "+v"(oc.e) : : "memory");
@@ -980,7 +1003,7 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
                 __builtin_amdgcn_s_waitcnt(0x0070);
             }
         }
-        asm_st32(my < mc.cnt ? (void *)(out + k0 + my) : (void *)sink, h);
+        asm_st32<kNT>(my < mc.cnt ? (void *)(out + k0 + my) : (void *)sink, h);
         mc = mD;
     };
 
@@ -1087,6 +1110,10 @@ hipError_t launch_sorted(const uint8_t *base, const uint64_t *off, uint64_t delt
         }
         if (var & 16) return (var & 8) ? launch_kernel<MODE, SORT, 24>(base, off, delta, nkeys, out, stream)
                                        : launch_kernel<MODE, SORT, 16>(base, off, delta, nkeys, out, stream);
+    }
+    if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_MD5) {
+        if (var & 64) return (var & 32) ? launch_kernel<MODE, SORT, 32 | 64>(base, off, delta, nkeys, out, stream)
+                                        : launch_kernel<MODE, SORT, 64>(base, off, delta, nkeys, out, stream);
     }
     if (var & 32) {
         if constexpr (has_mul_variant(MODE)) {

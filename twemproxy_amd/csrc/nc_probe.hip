@@ -12,6 +12,7 @@ constexpr int kProbeUnroll = 8;
 
 /* Each workgroup streams contiguous 16-byte pieces, kProbeUnroll loads in
  * flight per lane, and xors everything into one word so nothing is dead. */
+template <bool NT>
 __global__ __launch_bounds__(kProbeBlock) void probe_read_kernel(const uint4 *__restrict__ p, uint64_t n16,
                                                                  uint32_t *__restrict__ sink)
 {
@@ -23,7 +24,13 @@ __global__ __launch_bounds__(kProbeBlock) void probe_read_kernel(const uint4 *__
 #pragma unroll
         for (int u = 0; u < kProbeUnroll; u++) {
             const uint64_t i = base + (uint64_t)u * kProbeBlock;
-            v[u] = i < n16 ? p[i] : make_uint4(0, 0, 0, 0);
+            if constexpr (NT) {
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                v4u x = {0u, 0u, 0u, 0u};
+                if (i < n16) x = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p) + i);
+                v[u] = make_uint4(x.x, x.y, x.z, x.w);
+            }
+            else v[u] = i < n16 ? p[i] : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int u = 0; u < kProbeUnroll; u++) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
@@ -32,10 +39,8 @@ __global__ __launch_bounds__(kProbeBlock) void probe_read_kernel(const uint4 *__
     if ((threadIdx.x & 63u) == 0) atomicXor(&sink[blockIdx.x], acc);
 }
 
-} // namespace
-
-extern "C" rstatus_t nc_gpuhash_probe_read(const void *d_buf, uint64_t bytes, uint32_t *d_sink, void *stream,
-                                           int iters, float *avg_ms)
+template <bool NT>
+rstatus_t probe_read(const void *d_buf, uint64_t bytes, uint32_t *d_sink, void *stream, int iters, float *avg_ms)
 {
     if (d_buf == nullptr || d_sink == nullptr || avg_ms == nullptr || iters <= 0 || (bytes & 15u)) {
         errno = EINVAL;
@@ -60,11 +65,11 @@ extern "C" rstatus_t nc_gpuhash_probe_read(const void *d_buf, uint64_t bytes, ui
         errno = ENODEV;
         return NC_ERROR;
     }
-    hipLaunchKernelGGL(probe_read_kernel, dim3(grid), dim3(kProbeBlock), 0, st, (const uint4 *)d_buf, bytes / 16,
-                       d_sink);
+    hipLaunchKernelGGL(probe_read_kernel<NT>, dim3(grid), dim3(kProbeBlock), 0, st, (const uint4 *)d_buf,
+                       bytes / 16, d_sink);
     (void)hipEventRecord(a, st);
     for (int i = 0; i < iters; i++) {
-        hipLaunchKernelGGL(probe_read_kernel, dim3(grid), dim3(kProbeBlock), 0, st, (const uint4 *)d_buf,
+        hipLaunchKernelGGL(probe_read_kernel<NT>, dim3(grid), dim3(kProbeBlock), 0, st, (const uint4 *)d_buf,
                            bytes / 16, d_sink);
     }
     (void)hipEventRecord(b, st);
@@ -80,4 +85,18 @@ extern "C" rstatus_t nc_gpuhash_probe_read(const void *d_buf, uint64_t bytes, ui
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     return rc;
+}
+
+} // namespace
+
+extern "C" rstatus_t nc_gpuhash_probe_read(const void *d_buf, uint64_t bytes, uint32_t *d_sink, void *stream,
+                                           int iters, float *avg_ms)
+{
+    return probe_read<false>(d_buf, bytes, d_sink, stream, iters, avg_ms);
+}
+
+extern "C" rstatus_t nc_gpuhash_probe_read_nt(const void *d_buf, uint64_t bytes, uint32_t *d_sink, void *stream,
+                                              int iters, float *avg_ms)
+{
+    return probe_read<true>(d_buf, bytes, d_sink, stream, iters, avg_ms);
 }

@@ -150,19 +150,17 @@ def time_batch_device(hash_: int | str, keys, offsets, out, iters: int, stream=N
     return float(ms.value)
 
 
-def probe_read_gbs(buf, iters: int = 20, stream=None) -> float:
+def probe_read_gbs(buf, iters: int = 20, stream=None, nt: bool = False) -> float:
     """Same-run HBM read ceiling: GB/s of a STREAM-style 16-byte read over the
-    uint8 CUDA tensor `buf` (nc_gpuhash_probe_read)."""
+    uint8 CUDA tensor `buf` (nc_gpuhash_probe_read, or _nt for non-temporal loads)."""
     import torch
 
     nbytes = (buf.numel() // 16) * 16
     sink = torch.zeros(65536, dtype=torch.int32, device=buf.device)
     ms = ctypes.c_float(0.0)
-    L.check(
-        L.lib().nc_gpuhash_probe_read(buf.data_ptr(), nbytes, sink.data_ptr(), _stream_handle(stream), iters,
-                                      ctypes.byref(ms)),
-        "nc_gpuhash_probe_read",
-    )
+    name = "nc_gpuhash_probe_read_nt" if nt else "nc_gpuhash_probe_read"
+    L.check(getattr(L.lib(), name)(buf.data_ptr(), nbytes, sink.data_ptr(), _stream_handle(stream), iters,
+                                   ctypes.byref(ms)), name)
     return nbytes / (ms.value * 1e-3) / 1e9
 
 
