@@ -107,7 +107,9 @@ rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, const uint64_t
  * 0 off, 1..3 = 2..4 tiles ahead; bit 3: DIAGNOSTIC no-hash build, fnv1a_64
  * unsorted only, outputs are NOT hashes; bit 4: DIAGNOSTIC arithmetic offsets
  * for fixed 32-byte keys, fnv1a_64 unsorted only; bit 5: register-staged
- * pipeline, two tiles in flight; -1 = keep). */
+ * pipeline, two tiles in flight; bit 6: default cache policy on the key,
+ * offset and output streams instead of non-temporal, fnv1a_64 and md5 only;
+ * -1 = keep). */
 rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
 /* ---- 3b. host batches through a context (pinned staging, one stream per slot) ---- */

@@ -41,8 +41,8 @@ def gpu_hash(mode, keys_d, off_d):
                         (0, 0, 96), (7, 1, 96)],
                 ids=["persistent+sort", "persistent", "grid37+sort+shiftadd", "shiftadd+pf2",
                      "grid5+sort+pf2", "pf3", "grid3+sort+pf4", "regstage", "regstage+sort",
-                     "grid11+regstage+sort+shiftadd", "grid9+regstage", "nt", "nt+sort", "regstage+nt",
-                     "grid7+regstage+nt+sort"])
+                     "grid11+regstage+sort+shiftadd", "grid9+regstage", "cached", "cached+sort",
+                     "regstage+cached", "grid7+regstage+cached+sort"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)

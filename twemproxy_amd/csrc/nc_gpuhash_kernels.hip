@@ -66,6 +66,7 @@ static_assert(kOffTab % 16 == 0, "LDS carve must stay 16-byte aligned");
 
 struct LdsSrc {
     typedef uint32_t pos_t;
+    static constexpr bool kOverread = true; /* reads past a key stay inside LDS */
     const uint32_t *base; /* 16-byte aligned LDS slab, read as dwords */
     /* dwords i, i+1 (4-byte aligned): one ds_read2_b32 */
     __device__ __forceinline__ uint2 d2(uint32_t i) const { return make_uint2(base[i], base[i + 1]); }
@@ -74,6 +75,7 @@ struct LdsSrc {
 
 struct GlobalSrc {
     typedef uint64_t pos_t;
+    static constexpr bool kOverread = false; /* at most NC_GPUHASH_PAD past the last key */
     const uint32_t *base; /* 16-byte aligned key buffer */
     __device__ __forceinline__ uint2 d2(uint64_t i) const { return make_uint2(base[i], base[i + 1]); }
     __device__ __forceinline__ uint32_t d1(uint64_t i) const { return base[i]; }
@@ -338,14 +340,23 @@ __device__ __forceinline__ uint32_t hash_md5_dev(const Src &src, typename Src::p
         }
         nc_md5_block(s, w);
     }
-    /* final block(s): remaining rem bytes, 0x80, zeros, 64-bit bit length */
+    /* final block(s): remaining rem bytes, 0x80, zeros, 64-bit bit length.
+     * Word t is raw for t < q, the partial word | 0x80 pad for t == q, and 0
+     * after it (q = rem / 4). From LDS all 8 reads are unconditional (no
+     * per-lane branches; over-read bytes are masked off here). */
     const uint32_t rem = len & 63u;
+    const uint32_t q = rem >> 2;
+    const uint32_t sh = (rem & 3u) << 3;
+    const uint32_t keep = (1u << sh) - 1u; /* low rem%4 bytes of the partial word */
+    const uint32_t pad = 0x80u << sh;
 #pragma unroll
     for (int t = 0; t < 8; t++) {
         uint2 r = make_uint2(0u, 0u);
-        if (8u * t < rem) r = st.next8();
-        w[2 * t] = nc_md5_pad_word(r.x, 2 * t, rem);
-        w[2 * t + 1] = nc_md5_pad_word(r.y, 2 * t + 1, rem);
+        if constexpr (Src::kOverread) r = st.next8();
+        else if (8u * t < rem) r = st.next8();
+        const uint32_t t0 = 2u * t, t1 = 2u * t + 1u;
+        w[t0] = t0 < q ? r.x : (t0 == q ? ((r.x & keep) | pad) : 0u);
+        w[t1] = t1 < q ? r.y : (t1 == q ? ((r.y & keep) | pad) : 0u);
     }
     const uint64_t bits = (uint64_t)len << 3;
     if (rem >= 56) {
@@ -535,7 +546,8 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel(const uint8_t *__restri
     /* VAR bits 1-2: L2-prefetch distance code (0 off, 1..3 -> 2..4 tiles ahead) */
     constexpr uint32_t PD = ((VAR >> 1) & 3) ? (uint32_t)((VAR >> 1) & 3) + 1u : 0u;
     constexpr bool PF = PD != 0;
-    constexpr bool kNT = (VAR & 64) != 0;      /* variant bit 6: non-temporal key/offset/out streams */
+    constexpr bool kNT = (VAR & 64) == 0;      /* read-once streams are non-temporal; variant bit 6
+                                                  selects the default cache policy (A/B only) */
     constexpr int kAux = kNT ? 2 : 0;          /* global_load_lds cache-policy bits: 2 = nt */
     /* bounds are DMA'd DB tiles ahead: slab issue needs t+1, prefetch t+PD,
      * and both must be older than the previous iteration's prefetch */
@@ -906,7 +918,7 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
         return x < ntiles ? x : tile0;
     };
     uint32_t *sink = g_rs_sink + t;
-    constexpr bool kNT = (VAR & 64) != 0; /* variant bit 6: non-temporal streams */
+    constexpr bool kNT = (VAR & 64) == 0; /* nt streams unless variant bit 6 (default policy) */
 
     if constexpr (uses_crc_table<MODE>()) {
         tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
@@ -1024,7 +1036,9 @@ int g_grid_cap = -1; /* 0 = persistent: every resident workgroup slot once */
 int g_sort = -1;     /* 1 on, 0 off */
 int g_variant = 0;   /* bit 0: shift-add FNV multiply; bits 1-2: L2 prefetch distance code
                         (0 off, 1..3 -> 2..4 tiles ahead); bit 3: diagnostic no-hash build
-                        (fnv1a_64, unsorted; outputs are not hashes) */
+                        (fnv1a_64, unsorted; outputs are not hashes); bit 4: diagnostic
+                        arithmetic offsets; bit 5: register-staged kernel; bit 6: default
+                        cache policy instead of nt (fnv1a_64, md5) -- include/nc_gpuhash.h */
 
 int grid_cap()
 {
