@@ -38,11 +38,13 @@ def gpu_hash(mode, keys_d, off_d):
 
 @pytest.fixture(params=[(0, 1, 0), (0, 0, 0), (37, 1, 1), (0, 0, 3), (5, 1, 2), (0, 0, 4), (3, 1, 6),
                         (0, 0, 32), (0, 1, 32), (11, 1, 33), (9, 0, 32), (0, 0, 64), (0, 1, 64),
-                        (0, 0, 96), (7, 1, 96)],
+                        (0, 0, 96), (7, 1, 96), (0, 0, 128), (37, 0, 129), (0, 0, 384), (5, 0, 640),
+                        (0, 0, 896), (0, 0, 192)],
                 ids=["persistent+sort", "persistent", "grid37+sort+shiftadd", "shiftadd+pf2",
                      "grid5+sort+pf2", "pf3", "grid3+sort+pf4", "regstage", "regstage+sort",
                      "grid11+regstage+sort+shiftadd", "grid9+regstage", "cached", "cached+sort",
-                     "regstage+cached", "grid7+regstage+cached+sort"])
+                     "regstage+cached", "grid7+regstage+cached+sort", "wavering", "grid37+wavering+shiftadd",
+                     "wavering_4_1_2", "grid5+wavering_4_3_5", "wavering_5_2_3", "wavering+cached"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)
@@ -80,13 +82,20 @@ def test_misaligned_key_buffer(gpu, corpus, shift):
         np.testing.assert_array_equal(gpu_hash(m, kd, od), expected[m], err_msg=f"{t.HASH_NAMES[m]} shift {shift}")
 
 
-def test_offsets_not_starting_at_zero(gpu, oracle, corpus):
+@pytest.mark.parametrize("var", [0, 128])
+def test_offsets_not_starting_at_zero(gpu, oracle, corpus, var):
     keys, off, expected = corpus
-    lo, hi = 100, 700
     kd, od = to_dev(keys, off)
-    sub = od[lo: hi + 1].contiguous()  # absolute offsets into the same key buffer
-    for m in MODES:
-        np.testing.assert_array_equal(gpu_hash(m, kd, sub), expected[m][lo:hi])
+    L.lib().nc_gpuhash_set_tuning(0, 0, var)
+    try:
+        # absolute offsets into the same key buffer; lo = 101 leaves the offsets
+        # pointer 8-byte aligned only (the wave ring then hands over)
+        for lo, hi in ((100, 700), (101, 1000), (0, 1)):
+            sub = od[lo: hi + 1]
+            for m in MODES:
+                np.testing.assert_array_equal(gpu_hash(m, kd, sub), expected[m][lo:hi])
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
 
 
 def test_edge_batches(gpu, oracle):
@@ -195,7 +204,9 @@ def test_sort_and_grid_variants_agree_full_size(gpu):
     ref = None
     for grid, sort, var in ((0, 1, 0), (0, 0, 0), (2048, 1, 1), (4096, 0, 1), (1, 0, 0), (0, 0, 2), (0, 1, 2),
                             (3, 1, 3), (0, 0, 4), (7, 0, 6), (0, 0, 32), (0, 1, 32), (5, 1, 33), (13, 1, 32), (1024, 0, 32),
-                            (1536, 0, 32), (2048, 1, 32), (0, 0, 64), (0, 1, 64), (0, 0, 96), (1536, 1, 96)):
+                            (1536, 0, 32), (2048, 1, 32), (0, 0, 64), (0, 1, 64), (0, 0, 96), (1536, 1, 96),
+                            (0, 0, 128), (1, 0, 128), (7, 0, 384), (0, 0, 640), (2048, 0, 896), (0, 0, 129),
+                            (0, 0, 192)):
         L.lib().nc_gpuhash_set_tuning(grid, sort, var)
         out = t.hash_batch_device("fnv1a_64", kd, od)
         torch.cuda.synchronize()

@@ -246,6 +246,49 @@ __device__ __forceinline__ uint32_t hash_bytes(const Src &src, typename Src::pos
     return byte_final<MODE>(h);
 }
 
+/* Two keys of one lane hashed in one loop, so the two dependent chains
+ * interleave (ILP for the latency-bound byte recurrences). LDS only: the
+ * shorter key's stream reads on past its end (garbage bytes, never used). */
+template <int MODE, int VAR>
+__device__ __forceinline__ void hash_bytes_pair(const LdsSrc &src, uint32_t pa, uint32_t la, uint32_t pb,
+                                                uint32_t lb, const uint32_t *tab, uint32_t &ra, uint32_t &rb)
+{
+    ShiftK k{0u, 0u, 0u};
+    if constexpr ((VAR & 1) != 0) k = opaque_shifts();
+    QStream<LdsSrc> sa, sb;
+    sa.init(src, pa);
+    sb.init(src, pb);
+    uint32_t ha = byte_init<MODE>(), hb = ha;
+    const uint32_t na = la >> 3, nb = lb >> 3;
+    const uint32_t nmax = na > nb ? na : nb;
+    for (uint32_t i = 0; i < nmax; i++) {
+        const uint2 wa = sa.next8(), wb = sb.next8();
+        uint32_t xa = word_bytes<MODE, VAR>(ha, wa.x, tab, k);
+        uint32_t xb = word_bytes<MODE, VAR>(hb, wb.x, tab, k);
+        xa = word_bytes<MODE, VAR>(xa, wa.y, tab, k);
+        xb = word_bytes<MODE, VAR>(xb, wb.y, tab, k);
+        if (i < na) ha = xa;
+        if (i < nb) hb = xb;
+    }
+    /* tails: each key's stream is re-anchored on its tail */
+    auto tail = [&](uint32_t h, uint32_t p, uint32_t len) __attribute__((always_inline)) {
+        const uint32_t rem = len & 7u;
+        if (rem) {
+            QStream<LdsSrc> st;
+            st.init(src, p + (len & ~7u));
+            uint2 w = st.next8();
+            if (rem >= 4) {
+                h = word_bytes<MODE, VAR>(h, w.x, tab, k);
+                w.x = w.y;
+            }
+            for (uint32_t j = 0; j < (rem & 3u); j++) h = byte_step<MODE, VAR>(h, (w.x >> (8u * j)) & 0xffu, tab, k);
+        }
+        return byte_final<MODE>(h);
+    };
+    ra = tail(ha, pa, la);
+    rb = tail(hb, pb, lb);
+}
+
 /* ---------------- word-granular modes ---------------- */
 
 template <class Src>
@@ -1030,6 +1073,356 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
     asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
 }
 
+/* ---------------- wave-ring pipeline (variant bit 7; fused dispatch) ----------------
+ *
+ * Every wave runs its own pipeline over its own part of LDS: there is no
+ * barrier in the loop, so waves drift apart and the memory system sees a
+ * smooth request stream instead of lock-stepped bursts.
+ *
+ * A wave tile is 128 consecutive keys (lane l hashes keys k0+l and k0+64+l).
+ * Its offsets off[k0 .. k0+128] and its key slab come HBM -> LDS by LDS-DMA
+ * only, issued as inline asm so that hipcc's waitcnt pass never sees them
+ * (it would wait for a pending DMA before LDS reads). Iteration j issues
+ * exactly P + 4 VMEM instructions, in this order:
+ *   OFF(j+DO) : global_load_lds_dwordx4 (off[k0 .. k0+128), two per lane)
+ *               + global_load_lds_dword on lanes 0-1 (off[k0 + cnt])
+ *   SLAB(j+DS): P x global_load_lds_dwordx4 (1 KiB each; pieces the slab
+ *               does not need become one-lane dword DMAs into a dump word)
+ *   ST(j)     : 2 x global_store_dword (lanes without a key store to a sink)
+ * so both waits are constant vmcnt(N):
+ *   OFF(j+DS) landed, before SLAB(j+DS) is issued : N = (DO - DS)(P + 4)
+ *   SLAB(j) landed, before tile j is hashed        : N = DS (P + 4)
+ * The counter retires in order, so the first wait also retires every slab
+ * older than OFF(j+DS); DO >= 2 DS - 1 keeps SLAB(j+1) out of it. Extra VMEM
+ * instructions (the global-memory reader of a tile too long for its slab
+ * slot) only make the waits conservative; an instruction is never skipped,
+ * which is what would make them unsafe.
+ *
+ * DIST selects what is stored per key: the hash (kDistNone, the hashkit
+ * function), or server_pool_idx (src/nc_server.c:647-700): hash_tag trimming,
+ * hash 0 for an empty key, then ketama_dispatch / modula_dispatch over a
+ * continuum staged in LDS (kDistKetama / kDistModula), or the hash before
+ * dispatch (kDistPre, for continua too large for LDS). WPW waves per
+ * workgroup share the crc table and the continuum; each owns its ring.
+ */
+constexpr int kWrTile = 128;                         /* keys per wave tile */
+constexpr uint32_t kWrOffSlot = 8u * kWrTile + 16u;  /* off[k0 .. k0+128) + end bound, 16-aligned */
+constexpr int kDistNone = -1, kDistKetama = 0, kDistModula = 1, kDistPre = 3;
+
+/* server_pool_idx parameters of one launch (ignored for kDistNone) */
+struct WrDist {
+    const uint32_t *cont; /* struct continuum {index, value} pairs (src/nc_server.h:64-67) */
+    uint32_t ncont;
+    uint32_t tag;         /* hash_tag c0 | c1 << 8 | 1 << 16, or 0 for none */
+};
+
+template <int P, int DS, int DO>
+struct WrRing {
+    static_assert(DO > DS && DS >= 1 && DO >= 2 * DS - 1, "offsets must run far enough ahead of slabs");
+    static constexpr uint32_t NS = DS + 1;            /* slab slots: tiles j .. j+DS */
+    static constexpr uint32_t NO = DO + 1;            /* offset slots: tiles j .. j+DO */
+    static constexpr uint32_t kSlot = (uint32_t)P * 1024u;
+    static constexpr uint32_t kOffOffs = NS * kSlot;  /* slab over-reads land in the next slot / the offsets */
+    static constexpr uint32_t kOffDump = kOffOffs + NO * kWrOffSlot;
+    static constexpr uint32_t kBytes = kOffDump + 16u;
+    static constexpr int kWaitOff = (DO - DS) * (P + 4);
+    static constexpr int kWaitSlab = DS * (P + 4);
+};
+
+typedef __attribute__((address_space(3))) const void lds_cvoid_t;
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p)
+{
+    return (uint32_t)(uintptr_t)(lds_cvoid_t *)p;
+}
+
+/* LDS-DMA through M0 (saved and restored: M0 is compiler-reserved) */
+template <bool NT>
+__device__ __forceinline__ void glds16(const void *g, uint32_t lds)
+{
+    uint32_t keep;
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void glds4(const void *g, uint32_t lds)
+{
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm()
+{
+    static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t wr_count(uint64_t tile, uint64_t nkeys)
+{
+    const uint64_t left = nkeys - tile * (uint64_t)kWrTile;
+    return left < (uint64_t)kWrTile ? (uint32_t)left : (uint32_t)kWrTile;
+}
+
+/* {off[k0], off[k0+cnt]} + delta of the tile whose offsets are at ob, wave-uniform */
+__device__ __forceinline__ void wr_bounds(const uint32_t *ob, uint64_t delta, uint64_t &S, uint64_t &E)
+{
+    S = (((uint64_t)__builtin_amdgcn_readfirstlane(ob[1]) << 32) | __builtin_amdgcn_readfirstlane(ob[0])) + delta;
+    E = (((uint64_t)__builtin_amdgcn_readfirstlane(ob[2 * kWrTile + 1]) << 32) |
+         __builtin_amdgcn_readfirstlane(ob[2 * kWrTile])) + delta;
+}
+
+/* hash_tag trimming of server_pool_idx (src/nc_server.c:665-677): the first
+ * c0, then the first c1 after it; with at least one byte between them the
+ * key becomes the bytes in between. */
+template <class Src>
+__device__ __forceinline__ void tag_trim(const Src &src, typename Src::pos_t &p, uint32_t &len, uint32_t c0,
+                                         uint32_t c1)
+{
+    QStream<Src> st;
+    st.init(src, p);
+    uint32_t s = 0xffffffffu, e = 0xffffffffu;
+    for (uint32_t i = 0; i < len; i += 8u) {
+        const uint2 w = st.next8();
+#pragma unroll
+        for (uint32_t b = 0; b < 8u; b++) {
+            const uint32_t ch = ((b < 4u ? w.x : w.y) >> (8u * (b & 3u))) & 0xffu;
+            const bool in = i + b < len;
+            if (in && s != 0xffffffffu && e == 0xffffffffu && ch == c1) e = i + b;
+            if (in && s == 0xffffffffu && ch == c0) s = i + b;
+        }
+    }
+    if (s != 0xffffffffu && e != 0xffffffffu && e - s > 1u) {
+        p += s + 1u;
+        len = e - s - 1u;
+    }
+}
+
+/* ketama_dispatch (src/hashkit/nc_ketama.c:222-246): the first point whose
+ * value is >= hash, wrapping to the first point; c = {index, value} pairs */
+__device__ __forceinline__ uint32_t ketama_find(const uint32_t *c, uint32_t n, uint32_t h)
+{
+    uint32_t lo = 0, len = n;
+    while (len > 0u) {
+        const uint32_t half = len >> 1;
+        if (c[2u * (lo + half) + 1u] < h) {
+            lo += half + 1u;
+            len -= half + 1u;
+        } else {
+            len = half;
+        }
+    }
+    return c[2u * (lo == n ? 0u : lo)];
+}
+
+template <int MODE, int VAR, int DIST, class Src>
+__device__ __forceinline__ uint32_t key_value(const Src &src, typename Src::pos_t p, uint32_t len,
+                                              const uint32_t *tab, const WrDist &dist, const uint32_t *cont)
+{
+    if constexpr (DIST == kDistNone && (VAR & 8) != 0) {
+        return (uint32_t)p ^ len; /* DIAGNOSTIC ONLY: the memory pipeline without hashing */
+    } else if constexpr (DIST == kDistNone) {
+        return hash_key<MODE, VAR>(src, p, len, tab);
+    } else {
+        if (dist.tag != 0u) tag_trim(src, p, len, dist.tag & 0xffu, (dist.tag >> 8) & 0xffu);
+        uint32_t h = 0u; /* server_pool_hash: keylen 0 hashes to 0 (src/nc_server.c:639-641) */
+        if (len != 0u) h = hash_key<MODE, VAR>(src, p, len, tab);
+        if constexpr (DIST == kDistKetama) return ketama_find(cont, dist.ncont, h);
+        else if constexpr (DIST == kDistModula) return cont[2u * (h % dist.ncont)]; /* nc_modula.c:153 */
+        else return h;
+    }
+}
+
+template <int MODE, int DIST, int P, int DS, int DO, int WPW>
+constexpr uint32_t wr_lds_fixed()
+{
+    return (uint32_t)WPW * WrRing<P, DS, DO>::kBytes + (uses_crc_table<MODE>() ? 1024u : 0u);
+}
+
+template <int MODE, int VAR, int P, int DS, int DO, int DIST, int WPW>
+__global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__restrict__ keys_base,
+                                                              const uint64_t *__restrict__ off, uint64_t delta,
+                                                              uint64_t nkeys, uint32_t *__restrict__ out,
+                                                              uint64_t ntiles, WrDist dist)
+{
+    using R = WrRing<P, DS, DO>;
+    constexpr uint32_t NS = R::NS, NO = R::NO;
+    constexpr bool kNT = (VAR & 64) == 0;
+    constexpr uint32_t kTabOffs = (uint32_t)WPW * R::kBytes;
+    constexpr uint32_t kContOffs = wr_lds_fixed<MODE, DIST, P, DS, DO, WPW>();
+    extern __shared__ __attribute__((aligned(16))) uint8_t wr_lds[];
+
+    const uint32_t t = threadIdx.x;
+    const uint32_t lane = t & 63u;
+    const uint32_t wave = WPW == 1 ? 0u : __builtin_amdgcn_readfirstlane(t >> 6);
+    uint8_t *smem = wr_lds + wave * R::kBytes;
+    uint32_t *tab = reinterpret_cast<uint32_t *>(wr_lds + kTabOffs);
+    uint32_t *cont = reinterpret_cast<uint32_t *>(wr_lds + kContOffs);
+
+    /* shared set-up, before any DMA is in flight */
+    if constexpr (uses_crc_table<MODE>()) {
+        for (uint32_t i = t; i < 256u; i += 64u * WPW)
+            tab[i] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(i) : nc_crc32_entry(i);
+    }
+    if constexpr (DIST == kDistKetama || DIST == kDistModula) {
+        for (uint32_t i = t; i < 2u * dist.ncont; i += 64u * WPW) cont[i] = dist.cont[i];
+    }
+    if constexpr (WPW > 1) __syncthreads();
+
+    const uint64_t W = (uint64_t)gridDim.x * WPW;
+    const uint64_t tile0 = (uint64_t)blockIdx.x * WPW + wave;
+    if (tile0 >= ntiles) return;
+    uint32_t *sink = g_rs_sink + lane;
+    const uint32_t smem_lds = lds_addr(smem);
+
+    /* a VMEM instruction that moves one word nobody reads: keeps the
+     * per-iteration count fixed */
+    auto dummy = [&]() __attribute__((always_inline)) {
+        if (lane == 0u) glds4(off, smem_lds + R::kOffDump);
+    };
+    /* OFF(tile) into offset slot `oslot`: 2 instructions */
+    auto issue_off = [&](uint64_t tile, uint32_t oslot) __attribute__((always_inline)) {
+        if (tile >= ntiles) {
+            dummy();
+            dummy();
+            return;
+        }
+        const uint64_t k0 = tile * (uint64_t)kWrTile;
+        const uint64_t last_pair = (nkeys - 1u) & ~(uint64_t)1; /* pairs (p, p+1) stay <= nkeys */
+        uint64_t p = k0 + 2u * lane;
+        if (p > last_pair) p = last_pair;
+        const uint32_t dst = smem_lds + R::kOffOffs + oslot * kWrOffSlot;
+        glds16<kNT>(off + p, dst);
+        if (lane < 2u) {
+            const uint64_t e = k0 + wr_count(tile, nkeys);
+            glds4(reinterpret_cast<const uint32_t *>(off + e) + lane, dst + 8u * kWrTile);
+        }
+    };
+    /* SLAB(tile) into slab slot `sslot`: P instructions; OFF(tile) has landed */
+    auto issue_slab = [&](uint64_t tile, uint32_t oslot, uint32_t sslot) __attribute__((always_inline)) {
+        uint32_t nins = 0, nch = 0;
+        uint64_t S16 = 0;
+        if (tile < ntiles) {
+            uint64_t S, E;
+            wr_bounds(reinterpret_cast<const uint32_t *>(smem + R::kOffOffs + oslot * kWrOffSlot), delta, S, E);
+            S16 = S & ~(uint64_t)15;
+            const uint64_t span = E - S16;
+            if (span <= (uint64_t)R::kSlot) {
+                nch = (uint32_t)((span + 15u) >> 4);
+                nins = (nch + 63u) >> 6;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* earlier reads of the slot have retired */
+        const uint32_t dst = smem_lds + sslot * R::kSlot;
+#pragma unroll
+        for (int i = 0; i < P; i++) {
+            if ((uint32_t)i < nins) {
+                uint32_t c = 64u * (uint32_t)i + lane;
+                if (c >= nch) c = nch - 1u; /* stay inside the key buffer (+ NC_GPUHASH_PAD) */
+                glds16<kNT>(keys_base + S16 + 16u * c, dst + 1024u * (uint32_t)i);
+            } else {
+                dummy();
+            }
+        }
+    };
+
+    /* prologue: the steady-state queue, as if iterations -DO .. -1 had run */
+#pragma unroll
+    for (int jj = -DO; jj < 0; jj++) {
+        issue_off(tile0 + (uint64_t)(jj + DO) * W, (uint32_t)(jj + DO) % NO);
+        if (jj + DS >= 0) {
+            wait_vm<R::kWaitOff>();
+            issue_slab(tile0 + (uint64_t)(jj + DS) * W, (uint32_t)(jj + DS) % NO, (uint32_t)(jj + DS) % NS);
+        } else {
+#pragma unroll
+            for (int i = 0; i < P; i++) dummy();
+        }
+        dummy();
+        dummy();
+    }
+
+    for (uint32_t j = 0;; j++) {
+        const uint64_t tile = tile0 + (uint64_t)j * W;
+        if (tile >= ntiles) break;
+        issue_off(tile + (uint64_t)DO * W, (j + DO) % NO);
+        wait_vm<R::kWaitOff>();
+        issue_slab(tile + (uint64_t)DS * W, (j + DS) % NO, (j + DS) % NS);
+        wait_vm<R::kWaitSlab>();
+
+        const uint32_t *ob = reinterpret_cast<const uint32_t *>(smem + R::kOffOffs + (j % NO) * kWrOffSlot);
+        const uint8_t *slab = smem + (j % NS) * R::kSlot;
+        const uint32_t cnt = wr_count(tile, nkeys);
+        uint64_t S, E;
+        wr_bounds(ob, delta, S, E);
+        const uint64_t S16 = S & ~(uint64_t)15;
+        const bool in_lds = E - S16 <= (uint64_t)R::kSlot;
+        const uint64_t k0 = tile * (uint64_t)kWrTile;
+
+        uint32_t h[2];
+        constexpr bool kPair = (VAR & 512) != 0 && DIST == kDistNone && MODE != NC_GPUHASH_MD5 &&
+                               MODE != NC_GPUHASH_HSIEH && MODE != NC_GPUHASH_MURMUR && MODE != NC_GPUHASH_JENKINS;
+        if constexpr (kPair) {
+            if (in_lds) {
+                uint32_t len2[2], pos2[2];
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const uint32_t i = lane + 64u * (uint32_t)q;
+                    const uint32_t ie = i + 1u >= cnt ? (uint32_t)kWrTile : i + 1u;
+                    const uint32_t s = ob[2u * i];
+                    len2[q] = i < cnt ? ob[2u * ie] - s : 0u;
+                    pos2[q] = i < cnt ? s + (uint32_t)delta - (uint32_t)S16 : 0u;
+                }
+                LdsSrc src{reinterpret_cast<const uint32_t *>(slab)};
+                hash_bytes_pair<MODE, VAR>(src, pos2[0], len2[0], pos2[1], len2[1], tab, h[0], h[1]);
+                goto stores;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const uint32_t i = lane + 64u * (uint32_t)q;
+            const bool valid = i < cnt;
+            const uint32_t ie = i + 1u >= cnt ? (uint32_t)kWrTile : i + 1u; /* key cnt-1 ends at the end bound */
+            const uint32_t s = ob[2u * i];
+            const uint32_t e = ob[2u * ie];
+            const uint32_t len = valid ? e - s : 0u;
+            const uint32_t pos = valid ? s + (uint32_t)delta - (uint32_t)S16 : 0u;
+            if (in_lds) {
+                LdsSrc src{reinterpret_cast<const uint32_t *>(slab)};
+                h[q] = key_value<MODE, VAR, DIST>(src, pos, len, tab, dist, cont);
+            } else {
+                GlobalSrc src{reinterpret_cast<const uint32_t *>(keys_base)};
+                h[q] = key_value<MODE, VAR, DIST>(src, S16 + pos, len, tab, dist, cont);
+                /* retire the global reader's own loads before the paths
+                 * merge: a load still pending there makes hipcc wait
+                 * vmcnt(0) at the merge, draining the DMA ring */
+                __builtin_amdgcn_s_waitcnt(0x0070);
+            }
+        }
+    stores:
+        asm_st32<kNT>(lane < cnt ? (void *)(out + k0 + lane) : (void *)sink, h[0]);
+        asm_st32<kNT>(lane + 64u < cnt ? (void *)(out + k0 + 64u + lane) : (void *)sink, h[1]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
+}
+
+/* ketama / modula over pre-dispatch hashes, in place (continua too large
+ * for the fused kernel's LDS); the continuum is read through L2 */
+template <int DIST>
+__global__ __launch_bounds__(256) void nc_dispatch_kernel(const uint32_t *__restrict__ cont, uint32_t ncont,
+                                                          uint32_t *__restrict__ io, uint64_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
+        const uint32_t h = io[i];
+        io[i] = DIST == kDistKetama ? ketama_find(cont, ncont, h) : cont[2u * (h % ncont)];
+    }
+}
+
 /* ---------------- launch layer ---------------- */
 
 int g_grid_cap = -1; /* 0 = persistent: every resident workgroup slot once */
@@ -1151,6 +1544,105 @@ hipError_t launch_mode(const uint8_t *base, const uint64_t *off, uint64_t delta,
                 : launch_sorted<MODE, false>(base, off, delta, nkeys, out, stream, var);
 }
 
+/* One wave-ring launch: a persistent grid of every resident workgroup slot
+ * (occupancy cached per instantiation and LDS size) unless capped. */
+template <int MODE, int VAR, int P, int DS, int DO, int DIST, int WPW>
+hipError_t launch_wr(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                     hipStream_t stream, const WrDist &dist, size_t lds)
+{
+    void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist) =
+        nc_hash_kernel_wr<MODE, VAR, P, DS, DO, DIST, WPW>;
+    static size_t cached_lds = 0;
+    static int per_cu = 0;
+    if (per_cu == 0 || cached_lds != lds) {
+        if (lds > 65536u) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * WPW, lds) != hipSuccess || b <= 0) b = 1;
+        per_cu = b;
+        cached_lds = lds;
+    }
+    const uint64_t ntiles = (nkeys + kWrTile - 1) / kWrTile;
+    const uint64_t max_grid = (ntiles + WPW - 1) / WPW;
+    const int cap = grid_cap();
+    uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu;
+    if (grid > max_grid) grid = max_grid;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * WPW), lds, stream, base, off, delta, nkeys, out, ntiles,
+                       dist);
+    return hipGetLastError();
+}
+
+template <int MODE, int VAR, int P, int DS, int DO, int WPW = 1>
+hipError_t launch_wr_plain(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                           hipStream_t stream)
+{
+    const WrDist none{nullptr, 0u, 0u};
+    return launch_wr<MODE, VAR, P, DS, DO, kDistNone, WPW>(base, off, delta, nkeys, out, stream, none,
+                                                           wr_lds_fixed<MODE, kDistNone, P, DS, DO, WPW>());
+}
+
+/* EXPERIMENT (fnv1a_64 only): bit 11 = four waves per workgroup (one per
+ * SIMD), bit 12 = pair-interleaved hashing, bit 0 = shift-add multiply */
+template <int MODE, int VAR>
+hipError_t launch_wr_x(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                       hipStream_t stream, int var)
+{
+    const bool w4 = (var & 2048) != 0;
+    switch ((var >> 8) & 7) {
+    case 1: return w4 ? launch_wr_plain<MODE, VAR, 4, 1, 2, 4>(base, off, delta, nkeys, out, stream)
+                      : launch_wr_plain<MODE, VAR, 4, 1, 2, 1>(base, off, delta, nkeys, out, stream);
+    case 3: return w4 ? launch_wr_plain<MODE, VAR, 5, 2, 3, 4>(base, off, delta, nkeys, out, stream)
+                      : launch_wr_plain<MODE, VAR, 5, 2, 3, 1>(base, off, delta, nkeys, out, stream);
+    case 7: return w4 ? launch_wr_plain<MODE, VAR, 3, 1, 2, 4>(base, off, delta, nkeys, out, stream)
+                      : launch_wr_plain<MODE, VAR, 3, 1, 2, 1>(base, off, delta, nkeys, out, stream);
+    default: return w4 ? launch_wr_plain<MODE, VAR, 4, 2, 3, 4>(base, off, delta, nkeys, out, stream)
+                       : launch_wr_plain<MODE, VAR, 4, 2, 3, 1>(base, off, delta, nkeys, out, stream);
+    }
+}
+
+/* plain hashing on the wave ring; variant bits 8-10 pick the ring shape
+ * (P KiB slab slots, slabs DS and offsets DO tiles ahead) */
+template <int MODE, int VAR>
+hipError_t launch_wr_hash(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                          hipStream_t stream, int var)
+{
+    switch ((var >> 8) & 7) {
+    case 1: return launch_wr_plain<MODE, VAR, 4, 1, 2>(base, off, delta, nkeys, out, stream);
+    case 2: return launch_wr_plain<MODE, VAR, 4, 3, 5>(base, off, delta, nkeys, out, stream);
+    case 3: return launch_wr_plain<MODE, VAR, 5, 2, 3>(base, off, delta, nkeys, out, stream);
+    case 4: return launch_wr_plain<MODE, VAR, 6, 2, 3>(base, off, delta, nkeys, out, stream);
+    case 5: return launch_wr_plain<MODE, VAR, 5, 1, 2>(base, off, delta, nkeys, out, stream);
+    case 6: return launch_wr_plain<MODE, VAR, 3, 2, 3>(base, off, delta, nkeys, out, stream);
+    case 7: return launch_wr_plain<MODE, VAR, 3, 1, 2>(base, off, delta, nkeys, out, stream);
+    default: return launch_wr_plain<MODE, VAR, 4, 2, 3>(base, off, delta, nkeys, out, stream);
+    }
+}
+
+template <int MODE>
+hipError_t launch_wr_mode(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                          hipStream_t stream, int var)
+{
+    if constexpr (MODE == NC_GPUHASH_FNV1A_64) {
+        if (var & (2048 | 4096)) {
+            const int v = (var & 1) | ((var & 4096) ? 512 : 0);
+            switch (v) {
+            case 1: return launch_wr_x<MODE, 1>(base, off, delta, nkeys, out, stream, var);
+            case 512: return launch_wr_x<MODE, 512>(base, off, delta, nkeys, out, stream, var);
+            case 513: return launch_wr_x<MODE, 513>(base, off, delta, nkeys, out, stream, var);
+            default: return launch_wr_x<MODE, 0>(base, off, delta, nkeys, out, stream, var);
+            }
+        }
+        if (var & 8) { /* DIAGNOSTIC no-hash build: default and P5 ring shapes only */
+            if (((var >> 8) & 7) == 3) return launch_wr_plain<MODE, 8, 5, 2, 3>(base, off, delta, nkeys, out, stream);
+            if (((var >> 8) & 7) == 7) return launch_wr_plain<MODE, 8, 3, 1, 2>(base, off, delta, nkeys, out, stream);
+            return launch_wr_plain<MODE, 8, 4, 2, 3>(base, off, delta, nkeys, out, stream);
+        }
+    }
+    if constexpr (has_mul_variant(MODE)) { /* shift-add multiply: default ring shape only */
+        if (var & 1) return launch_wr_plain<MODE, 1, 4, 2, 3>(base, off, delta, nkeys, out, stream);
+    }
+    return launch_wr_hash<MODE, 0>(base, off, delta, nkeys, out, stream, var);
+}
+
 hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
                   hipStream_t stream)
 {
@@ -1158,6 +1650,29 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
     const uint8_t *base = reinterpret_cast<const uint8_t *>(kp & ~(uintptr_t)15);
     const uint64_t delta = (uint64_t)(kp & 15u);
     const bool sort = sort_enabled();
+    /* the wave ring DMAs offsets 16 bytes per lane: it needs 16-byte aligned
+     * offsets (any other alignment takes the workgroup pipeline) */
+    if ((g_variant & 128) != 0 && (reinterpret_cast<uintptr_t>(d_off) & 15u) == 0) {
+        switch (mode) {
+#define NC_WCASE(M) \
+    case M: return launch_wr_mode<M>(base, d_off, delta, nkeys, d_out, stream, g_variant);
+            NC_WCASE(NC_GPUHASH_ONE_AT_A_TIME)
+            NC_WCASE(NC_GPUHASH_MD5)
+            NC_WCASE(NC_GPUHASH_CRC16)
+            NC_WCASE(NC_GPUHASH_CRC32)
+            NC_WCASE(NC_GPUHASH_CRC32A)
+            NC_WCASE(NC_GPUHASH_FNV1_64)
+            NC_WCASE(NC_GPUHASH_FNV1A_64)
+            NC_WCASE(NC_GPUHASH_FNV1_32)
+            NC_WCASE(NC_GPUHASH_FNV1A_32)
+            NC_WCASE(NC_GPUHASH_HSIEH)
+            NC_WCASE(NC_GPUHASH_MURMUR)
+            NC_WCASE(NC_GPUHASH_JENKINS)
+#undef NC_WCASE
+        default:
+            return hipErrorInvalidValue;
+        }
+    }
     switch (mode) {
 #define NC_CASE(M) \
     case M: return launch_mode<M>(base, d_off, delta, nkeys, d_out, stream, sort, g_variant);
