@@ -39,12 +39,13 @@ def gpu_hash(mode, keys_d, off_d):
 @pytest.fixture(params=[(0, 1, 0), (0, 0, 0), (37, 1, 1), (0, 0, 3), (5, 1, 2), (0, 0, 4), (3, 1, 6),
                         (0, 0, 32), (0, 1, 32), (11, 1, 33), (9, 0, 32), (0, 0, 64), (0, 1, 64),
                         (0, 0, 96), (7, 1, 96), (0, 0, 128), (37, 0, 129), (0, 0, 384), (5, 0, 640),
-                        (0, 0, 896), (0, 0, 192)],
+                        (0, 0, 896), (0, 0, 192), (0, 0, 2432 | 4096), (3, 0, 3968 | 4096 | 16384)],
                 ids=["persistent+sort", "persistent", "grid37+sort+shiftadd", "shiftadd+pf2",
                      "grid5+sort+pf2", "pf3", "grid3+sort+pf4", "regstage", "regstage+sort",
                      "grid11+regstage+sort+shiftadd", "grid9+regstage", "cached", "cached+sort",
                      "regstage+cached", "grid7+regstage+cached+sort", "wavering", "grid37+wavering+shiftadd",
-                     "wavering_4_1_2", "grid5+wavering_4_3_5", "wavering_5_2_3", "wavering+cached"])
+                     "wavering_4_1_2", "grid5+wavering_4_3_5", "wavering_5_2_3", "wavering+cached",
+                     "wavering_w4_pair", "grid3+wavering_3_1_2_w4_pair_pin"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)

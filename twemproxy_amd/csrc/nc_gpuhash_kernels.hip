@@ -86,13 +86,17 @@ struct GlobalSrc {
  * v_alignbyte_b32; one ds_read2_b32 per 8 bytes, no selects. Reads at most
  * 14 bytes past the end of the string (covered by the staged look-ahead
  * piece / NC_GPUHASH_PAD). */
-template <class Src>
+template <class Src, bool kDeep = false>
 struct QStream {
+    /* kDeep (LDS only): reads run two steps ahead, so a step never waits for
+     * the read the previous step issued */
+    static constexpr bool D2 = kDeep && Src::kOverread;
     Src src;
     typename Src::pos_t di;
     uint32_t sh;
     uint32_t prev;
-    uint2 ahead; /* dwords di+1, di+2, read one step early */
+    uint2 ahead;  /* dwords di+1, di+2, read one step early */
+    uint2 ahead2; /* dwords di+3, di+4 (D2 only) */
 
     __device__ __forceinline__ void init(const Src &s, typename Src::pos_t p)
     {
@@ -101,6 +105,7 @@ struct QStream {
         sh = (uint32_t)p & 3u;
         prev = src.d1(di);
         ahead = src.d2(di + 1);
+        if constexpr (D2) ahead2 = src.d2(di + 3);
     }
     /* next 8 bytes as two words; the read for the following 8 is issued now
      * (it may touch up to 22 bytes past the string: inside the staged
@@ -109,7 +114,13 @@ struct QStream {
     {
         const uint2 d = ahead;
         di += 2;
-        ahead = src.d2(di + 1);
+        if constexpr (D2) {
+            ahead = ahead2;
+            ahead2 = src.d2(di + 3);
+            asm volatile("" ::: "memory"); /* keep the read here, not at its use */
+        } else {
+            ahead = src.d2(di + 1);
+        }
         uint2 r;
         r.x = __builtin_amdgcn_alignbyte(d.x, prev, sh);
         r.y = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
@@ -222,7 +233,7 @@ __device__ __forceinline__ uint32_t hash_bytes(const Src &src, typename Src::pos
 {
     ShiftK k{0u, 0u, 0u};
     if constexpr ((VAR & 1) != 0) k = opaque_shifts();
-    QStream<Src> st;
+    QStream<Src, (VAR & 1024) != 0> st;
     st.init(src, p);
     uint32_t h = byte_init<MODE>();
     const uint32_t n8 = len >> 3;
@@ -255,7 +266,7 @@ __device__ __forceinline__ void hash_bytes_pair(const LdsSrc &src, uint32_t pa, 
 {
     ShiftK k{0u, 0u, 0u};
     if constexpr ((VAR & 1) != 0) k = opaque_shifts();
-    QStream<LdsSrc> sa, sb;
+    QStream<LdsSrc, (VAR & 1024) != 0> sa, sb;
     sa.init(src, pa);
     sb.init(src, pb);
     uint32_t ha = byte_init<MODE>(), hb = ha;
@@ -263,10 +274,16 @@ __device__ __forceinline__ void hash_bytes_pair(const LdsSrc &src, uint32_t pa, 
     const uint32_t nmax = na > nb ? na : nb;
     for (uint32_t i = 0; i < nmax; i++) {
         const uint2 wa = sa.next8(), wb = sb.next8();
-        uint32_t xa = word_bytes<MODE, VAR>(ha, wa.x, tab, k);
-        uint32_t xb = word_bytes<MODE, VAR>(hb, wb.x, tab, k);
-        xa = word_bytes<MODE, VAR>(xa, wa.y, tab, k);
-        xb = word_bytes<MODE, VAR>(xb, wb.y, tab, k);
+        uint32_t xa = ha, xb = hb;
+        /* byte-granular alternation: in-order issue overlaps the two chains
+         * only if their steps alternate in the instruction stream */
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint32_t va = ((b < 4 ? wa.x : wa.y) >> (8 * (b & 3))) & 0xffu;
+            const uint32_t vb = ((b < 4 ? wb.x : wb.y) >> (8 * (b & 3))) & 0xffu;
+            xa = byte_step<MODE, VAR>(xa, va, tab, k);
+            xb = byte_step<MODE, VAR>(xb, vb, tab, k);
+        }
         if (i < na) ha = xa;
         if (i < nb) hb = xb;
     }
@@ -411,6 +428,65 @@ __device__ __forceinline__ uint32_t hash_md5_dev(const Src &src, typename Src::p
     w[15] = (uint32_t)(bits >> 32);
     nc_md5_block(s, w);
     return s[0]; /* digest bytes 0..3 little-endian (nc_md5.c:317-320) */
+}
+
+/* Message words of block `blk` of a key of `len` bytes read from `st`: the
+ * key's bytes, then 0x80, zeros and, in its last block, the bit length
+ * (src/hashkit/nc_md5.c:245-274). LDS only: the reads run past the key. */
+__device__ __forceinline__ void md5_words(QStream<LdsSrc> &st, uint32_t w[16], uint32_t len, uint32_t blk)
+{
+    const int32_t rem = (int32_t)len - 64 * (int32_t)blk; /* message bytes from the block start */
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint2 r = st.next8();
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t v = h ? r.y : r.x;
+            const int32_t nb = rem - (8 * t + 4 * h); /* message bytes in this word */
+            const uint32_t part = nb <= 0 ? 0u : (v & (0xffffffffu >> (32u - 8u * (uint32_t)nb)));
+            const uint32_t pad = (nb >= 0 && nb < 4) ? (0x80u << (8u * (uint32_t)nb)) : 0u;
+            w[2 * t + h] = nb >= 4 ? v : (part | pad);
+        }
+    }
+    if (blk == (len + 8u) / 64u) { /* the last block */
+        w[14] = len << 3;
+        w[15] = len >> 29;
+    }
+}
+
+/* md5 of a lane's two keys with their blocks interleaved step by step
+ * (nc_md5_block2): two independent chains per lane instead of one. */
+__device__ __forceinline__ void hash_md5_pair(const LdsSrc &src, uint32_t pa, uint32_t la, uint32_t pb,
+                                              uint32_t lb, uint32_t &ra, uint32_t &rb)
+{
+    QStream<LdsSrc> sa, sb;
+    sa.init(src, pa);
+    sb.init(src, pb);
+    uint32_t A[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
+    uint32_t B[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
+    const uint32_t na = (la + 8u) / 64u + 1u, nb = (lb + 8u) / 64u + 1u;
+    const uint32_t n = na > nb ? na : nb;
+    for (uint32_t blk = 0; blk < n; blk++) {
+        uint32_t wa[16], wb[16];
+        md5_words(sa, wa, la, blk);
+        md5_words(sb, wb, lb, blk);
+        uint32_t ta[4] = {A[0], A[1], A[2], A[3]}, tb[4] = {B[0], B[1], B[2], B[3]};
+        nc_md5_block2(ta, wa, tb, wb);
+        if (blk < na) {
+            A[0] = ta[0];
+            A[1] = ta[1];
+            A[2] = ta[2];
+            A[3] = ta[3];
+        }
+        if (blk < nb) {
+            B[0] = tb[0];
+            B[1] = tb[1];
+            B[2] = tb[2];
+            B[3] = tb[3];
+        }
+    }
+    ra = A[0]; /* digest bytes 0..3 little-endian (nc_md5.c:317-320) */
+    rb = B[0];
 }
 
 template <int MODE, int VAR, class Src>
@@ -580,8 +656,16 @@ __device__ __forceinline__ void read_bounds(const uint8_t *slot, uint64_t delta,
  * keys_base is 16-byte aligned; key i is keys_base[off[i]+delta, off[i+1]+delta)
  * and keys_base stays readable NC_GPUHASH_PAD bytes past the last key.
  */
+/* minimum waves per SIMD (1: no register cap). Capping md5 at 64 VGPRs for
+ * eight waves per SIMD spilled to scratch and ran 8 % slower on C3. */
+template <int MODE>
+constexpr int kMinWaves()
+{
+    return 1;
+}
+
 template <int MODE, bool SORT, int VAR>
-__global__ __launch_bounds__(kBlock) void nc_hash_kernel(const uint8_t *__restrict__ keys_base,
+__global__ __launch_bounds__(kBlock, kMinWaves<MODE>()) void nc_hash_kernel(const uint8_t *__restrict__ keys_base,
                                                          const uint64_t *__restrict__ off, uint64_t delta,
                                                          uint64_t nkeys, uint32_t *__restrict__ out,
                                                          uint64_t ntiles)
@@ -1105,8 +1189,7 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
  * dispatch (kDistPre, for continua too large for LDS). WPW waves per
  * workgroup share the crc table and the continuum; each owns its ring.
  */
-constexpr int kWrTile = 128;                         /* keys per wave tile */
-constexpr uint32_t kWrOffSlot = 8u * kWrTile + 16u;  /* off[k0 .. k0+128) + end bound, 16-aligned */
+constexpr int kWrTile = 128; /* keys per wave tile (64: one key per lane, the short-key shape) */
 constexpr int kDistNone = -1, kDistKetama = 0, kDistModula = 1, kDistPre = 3;
 
 /* server_pool_idx parameters of one launch (ignored for kDistNone) */
@@ -1116,17 +1199,20 @@ struct WrDist {
     uint32_t tag;         /* hash_tag c0 | c1 << 8 | 1 << 16, or 0 for none */
 };
 
-template <int P, int DS, int DO>
+template <int P, int DS, int DO, int TK = kWrTile>
 struct WrRing {
     static_assert(DO > DS && DS >= 1 && DO >= 2 * DS - 1, "offsets must run far enough ahead of slabs");
+    static_assert(TK == 64 || TK == 128, "a wave tile is one or two keys per lane");
+    static constexpr uint32_t kOffSlot = 8u * TK + 16u;  /* off[k0 .. k0+TK) + end bound, 16-aligned */
+    static constexpr int NST = TK / 64;                  /* output stores per tile */
     static constexpr uint32_t NS = DS + 1;            /* slab slots: tiles j .. j+DS */
     static constexpr uint32_t NO = DO + 1;            /* offset slots: tiles j .. j+DO */
     static constexpr uint32_t kSlot = (uint32_t)P * 1024u;
     static constexpr uint32_t kOffOffs = NS * kSlot;  /* slab over-reads land in the next slot / the offsets */
-    static constexpr uint32_t kOffDump = kOffOffs + NO * kWrOffSlot;
+    static constexpr uint32_t kOffDump = kOffOffs + NO * kOffSlot;
     static constexpr uint32_t kBytes = kOffDump + 16u;
-    static constexpr int kWaitOff = (DO - DS) * (P + 4);
-    static constexpr int kWaitSlab = DS * (P + 4);
+    static constexpr int kWaitOff = (DO - DS) * (P + 2 + NST);
+    static constexpr int kWaitSlab = DS * (P + 2 + NST);
 };
 
 typedef __attribute__((address_space(3))) const void lds_cvoid_t;
@@ -1164,18 +1250,20 @@ __device__ __forceinline__ void wait_vm()
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+template <int TK>
 __device__ __forceinline__ uint32_t wr_count(uint64_t tile, uint64_t nkeys)
 {
-    const uint64_t left = nkeys - tile * (uint64_t)kWrTile;
-    return left < (uint64_t)kWrTile ? (uint32_t)left : (uint32_t)kWrTile;
+    const uint64_t left = nkeys - tile * (uint64_t)TK;
+    return left < (uint64_t)TK ? (uint32_t)left : (uint32_t)TK;
 }
 
 /* {off[k0], off[k0+cnt]} + delta of the tile whose offsets are at ob, wave-uniform */
+template <int TK>
 __device__ __forceinline__ void wr_bounds(const uint32_t *ob, uint64_t delta, uint64_t &S, uint64_t &E)
 {
     S = (((uint64_t)__builtin_amdgcn_readfirstlane(ob[1]) << 32) | __builtin_amdgcn_readfirstlane(ob[0])) + delta;
-    E = (((uint64_t)__builtin_amdgcn_readfirstlane(ob[2 * kWrTile + 1]) << 32) |
-         __builtin_amdgcn_readfirstlane(ob[2 * kWrTile])) + delta;
+    E = (((uint64_t)__builtin_amdgcn_readfirstlane(ob[2 * TK + 1]) << 32) |
+         __builtin_amdgcn_readfirstlane(ob[2 * TK])) + delta;
 }
 
 /* hash_tag trimming of server_pool_idx (src/nc_server.c:665-677): the first
@@ -1239,23 +1327,24 @@ __device__ __forceinline__ uint32_t key_value(const Src &src, typename Src::pos_
     }
 }
 
-template <int MODE, int DIST, int P, int DS, int DO, int WPW>
+template <int MODE, int DIST, int P, int DS, int DO, int WPW, int TK = kWrTile>
 constexpr uint32_t wr_lds_fixed()
 {
-    return (uint32_t)WPW * WrRing<P, DS, DO>::kBytes + (uses_crc_table<MODE>() ? 1024u : 0u);
+    return (uint32_t)WPW * WrRing<P, DS, DO, TK>::kBytes + (uses_crc_table<MODE>() ? 1024u : 0u);
 }
 
-template <int MODE, int VAR, int P, int DS, int DO, int DIST, int WPW>
+template <int MODE, int VAR, int P, int DS, int DO, int DIST, int WPW, int TK = kWrTile>
 __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__restrict__ keys_base,
                                                               const uint64_t *__restrict__ off, uint64_t delta,
                                                               uint64_t nkeys, uint32_t *__restrict__ out,
                                                               uint64_t ntiles, WrDist dist)
 {
-    using R = WrRing<P, DS, DO>;
+    using R = WrRing<P, DS, DO, TK>;
     constexpr uint32_t NS = R::NS, NO = R::NO;
+    constexpr uint32_t kWrOffSlot = R::kOffSlot;
     constexpr bool kNT = (VAR & 64) == 0;
     constexpr uint32_t kTabOffs = (uint32_t)WPW * R::kBytes;
-    constexpr uint32_t kContOffs = wr_lds_fixed<MODE, DIST, P, DS, DO, WPW>();
+    constexpr uint32_t kContOffs = wr_lds_fixed<MODE, DIST, P, DS, DO, WPW, TK>();
     extern __shared__ __attribute__((aligned(16))) uint8_t wr_lds[];
 
     const uint32_t t = threadIdx.x;
@@ -1282,26 +1371,28 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
     const uint32_t smem_lds = lds_addr(smem);
 
     /* a VMEM instruction that moves one word nobody reads: keeps the
-     * per-iteration count fixed */
-    auto dummy = [&]() __attribute__((always_inline)) {
-        if (lane == 0u) glds4(off, smem_lds + R::kOffDump);
+     * per-iteration count fixed. `src` is a word the wave touches anyway
+     * (its own slab or offsets), so the dummies of all waves do not pile
+     * onto one L2 line. */
+    auto dummy = [&](const void *src) __attribute__((always_inline)) {
+        if (lane == 0u) glds4(src, smem_lds + R::kOffDump);
     };
     /* OFF(tile) into offset slot `oslot`: 2 instructions */
     auto issue_off = [&](uint64_t tile, uint32_t oslot) __attribute__((always_inline)) {
         if (tile >= ntiles) {
-            dummy();
-            dummy();
+            dummy(off + nkeys);
+            dummy(off + nkeys);
             return;
         }
-        const uint64_t k0 = tile * (uint64_t)kWrTile;
+        const uint64_t k0 = tile * (uint64_t)TK;
         const uint64_t last_pair = (nkeys - 1u) & ~(uint64_t)1; /* pairs (p, p+1) stay <= nkeys */
         uint64_t p = k0 + 2u * lane;
         if (p > last_pair) p = last_pair;
         const uint32_t dst = smem_lds + R::kOffOffs + oslot * kWrOffSlot;
-        glds16<kNT>(off + p, dst);
+        if (TK == 128 || lane < (uint32_t)TK / 2u) glds16<kNT>(off + p, dst);
         if (lane < 2u) {
-            const uint64_t e = k0 + wr_count(tile, nkeys);
-            glds4(reinterpret_cast<const uint32_t *>(off + e) + lane, dst + 8u * kWrTile);
+            const uint64_t e = k0 + wr_count<TK>(tile, nkeys);
+            glds4(reinterpret_cast<const uint32_t *>(off + e) + lane, dst + 8u * TK);
         }
     };
     /* SLAB(tile) into slab slot `sslot`: P instructions; OFF(tile) has landed */
@@ -1310,7 +1401,7 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
         uint64_t S16 = 0;
         if (tile < ntiles) {
             uint64_t S, E;
-            wr_bounds(reinterpret_cast<const uint32_t *>(smem + R::kOffOffs + oslot * kWrOffSlot), delta, S, E);
+            wr_bounds<TK>(reinterpret_cast<const uint32_t *>(smem + R::kOffOffs + oslot * kWrOffSlot), delta, S, E);
             S16 = S & ~(uint64_t)15;
             const uint64_t span = E - S16;
             if (span <= (uint64_t)R::kSlot) {
@@ -1327,7 +1418,7 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
                 if (c >= nch) c = nch - 1u; /* stay inside the key buffer (+ NC_GPUHASH_PAD) */
                 glds16<kNT>(keys_base + S16 + 16u * c, dst + 1024u * (uint32_t)i);
             } else {
-                dummy();
+                dummy(keys_base + S16);
             }
         }
     };
@@ -1341,10 +1432,10 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
             issue_slab(tile0 + (uint64_t)(jj + DS) * W, (uint32_t)(jj + DS) % NO, (uint32_t)(jj + DS) % NS);
         } else {
 #pragma unroll
-            for (int i = 0; i < P; i++) dummy();
+            for (int i = 0; i < P; i++) dummy(off + nkeys);
         }
-        dummy();
-        dummy();
+#pragma unroll
+        for (int i = 0; i < R::NST; i++) dummy(off + nkeys);
     }
 
     for (uint32_t j = 0;; j++) {
@@ -1357,37 +1448,40 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
 
         const uint32_t *ob = reinterpret_cast<const uint32_t *>(smem + R::kOffOffs + (j % NO) * kWrOffSlot);
         const uint8_t *slab = smem + (j % NS) * R::kSlot;
-        const uint32_t cnt = wr_count(tile, nkeys);
+        const uint32_t cnt = wr_count<TK>(tile, nkeys);
         uint64_t S, E;
-        wr_bounds(ob, delta, S, E);
+        wr_bounds<TK>(ob, delta, S, E);
         const uint64_t S16 = S & ~(uint64_t)15;
         const bool in_lds = E - S16 <= (uint64_t)R::kSlot;
-        const uint64_t k0 = tile * (uint64_t)kWrTile;
+        const uint64_t k0 = tile * (uint64_t)TK;
 
-        uint32_t h[2];
-        constexpr bool kPair = (VAR & 512) != 0 && DIST == kDistNone && MODE != NC_GPUHASH_MD5 &&
-                               MODE != NC_GPUHASH_HSIEH && MODE != NC_GPUHASH_MURMUR && MODE != NC_GPUHASH_JENKINS;
+        uint32_t h[R::NST];
+        constexpr bool kPair = TK == 128 && (VAR & 512) != 0 && DIST == kDistNone && MODE != NC_GPUHASH_HSIEH &&
+                               MODE != NC_GPUHASH_MURMUR && MODE != NC_GPUHASH_JENKINS;
         if constexpr (kPair) {
             if (in_lds) {
                 uint32_t len2[2], pos2[2];
 #pragma unroll
                 for (int q = 0; q < 2; q++) {
                     const uint32_t i = lane + 64u * (uint32_t)q;
-                    const uint32_t ie = i + 1u >= cnt ? (uint32_t)kWrTile : i + 1u;
+                    const uint32_t ie = i + 1u >= cnt ? (uint32_t)TK : i + 1u;
                     const uint32_t s = ob[2u * i];
                     len2[q] = i < cnt ? ob[2u * ie] - s : 0u;
                     pos2[q] = i < cnt ? s + (uint32_t)delta - (uint32_t)S16 : 0u;
                 }
                 LdsSrc src{reinterpret_cast<const uint32_t *>(slab)};
-                hash_bytes_pair<MODE, VAR>(src, pos2[0], len2[0], pos2[1], len2[1], tab, h[0], h[1]);
+                if constexpr (MODE == NC_GPUHASH_MD5)
+                    hash_md5_pair(src, pos2[0], len2[0], pos2[1], len2[1], h[0], h[1]);
+                else
+                    hash_bytes_pair<MODE, VAR>(src, pos2[0], len2[0], pos2[1], len2[1], tab, h[0], h[1]);
                 goto stores;
             }
         }
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
+        for (int q = 0; q < R::NST; q++) {
             const uint32_t i = lane + 64u * (uint32_t)q;
             const bool valid = i < cnt;
-            const uint32_t ie = i + 1u >= cnt ? (uint32_t)kWrTile : i + 1u; /* key cnt-1 ends at the end bound */
+            const uint32_t ie = i + 1u >= cnt ? (uint32_t)TK : i + 1u; /* key cnt-1 ends at the end bound */
             const uint32_t s = ob[2u * i];
             const uint32_t e = ob[2u * ie];
             const uint32_t len = valid ? e - s : 0u;
@@ -1405,8 +1499,11 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
             }
         }
     stores:
-        asm_st32<kNT>(lane < cnt ? (void *)(out + k0 + lane) : (void *)sink, h[0]);
-        asm_st32<kNT>(lane + 64u < cnt ? (void *)(out + k0 + 64u + lane) : (void *)sink, h[1]);
+#pragma unroll
+        for (int q = 0; q < R::NST; q++) {
+            const uint32_t i = lane + 64u * (uint32_t)q;
+            asm_st32<kNT>(i < cnt ? (void *)(out + k0 + i) : (void *)sink, h[q]);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
 }
@@ -1546,12 +1643,12 @@ hipError_t launch_mode(const uint8_t *base, const uint64_t *off, uint64_t delta,
 
 /* One wave-ring launch: a persistent grid of every resident workgroup slot
  * (occupancy cached per instantiation and LDS size) unless capped. */
-template <int MODE, int VAR, int P, int DS, int DO, int DIST, int WPW>
+template <int MODE, int VAR, int P, int DS, int DO, int DIST, int WPW, int TK = kWrTile>
 hipError_t launch_wr(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                      hipStream_t stream, const WrDist &dist, size_t lds)
 {
     void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist) =
-        nc_hash_kernel_wr<MODE, VAR, P, DS, DO, DIST, WPW>;
+        nc_hash_kernel_wr<MODE, VAR, P, DS, DO, DIST, WPW, TK>;
     static size_t cached_lds = 0;
     static int per_cu = 0;
     if (per_cu == 0 || cached_lds != lds) {
@@ -1561,7 +1658,7 @@ hipError_t launch_wr(const uint8_t *base, const uint64_t *off, uint64_t delta, u
         per_cu = b;
         cached_lds = lds;
     }
-    const uint64_t ntiles = (nkeys + kWrTile - 1) / kWrTile;
+    const uint64_t ntiles = (nkeys + TK - 1) / TK;
     const uint64_t max_grid = (ntiles + WPW - 1) / WPW;
     const int cap = grid_cap();
     uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu;
@@ -1571,13 +1668,13 @@ hipError_t launch_wr(const uint8_t *base, const uint64_t *off, uint64_t delta, u
     return hipGetLastError();
 }
 
-template <int MODE, int VAR, int P, int DS, int DO, int WPW = 1>
+template <int MODE, int VAR, int P, int DS, int DO, int WPW = 1, int TK = kWrTile>
 hipError_t launch_wr_plain(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                            hipStream_t stream)
 {
     const WrDist none{nullptr, 0u, 0u};
-    return launch_wr<MODE, VAR, P, DS, DO, kDistNone, WPW>(base, off, delta, nkeys, out, stream, none,
-                                                           wr_lds_fixed<MODE, kDistNone, P, DS, DO, WPW>());
+    return launch_wr<MODE, VAR, P, DS, DO, kDistNone, WPW, TK>(base, off, delta, nkeys, out, stream, none,
+                                                               wr_lds_fixed<MODE, kDistNone, P, DS, DO, WPW, TK>());
 }
 
 /* EXPERIMENT (fnv1a_64 only): bit 11 = four waves per workgroup (one per
@@ -1587,6 +1684,18 @@ hipError_t launch_wr_x(const uint8_t *base, const uint64_t *off, uint64_t delta,
                        hipStream_t stream, int var)
 {
     const bool w4 = (var & 2048) != 0;
+    if (var & 8192) { /* 64-key tiles, one key per lane */
+        switch ((var >> 8) & 7) {
+        case 1: return w4 ? launch_wr_plain<MODE, VAR, 2, 1, 2, 4, 64>(base, off, delta, nkeys, out, stream)
+                          : launch_wr_plain<MODE, VAR, 2, 1, 2, 1, 64>(base, off, delta, nkeys, out, stream);
+        case 3: return w4 ? launch_wr_plain<MODE, VAR, 3, 2, 3, 4, 64>(base, off, delta, nkeys, out, stream)
+                          : launch_wr_plain<MODE, VAR, 3, 2, 3, 1, 64>(base, off, delta, nkeys, out, stream);
+        case 7: return w4 ? launch_wr_plain<MODE, VAR, 2, 3, 5, 4, 64>(base, off, delta, nkeys, out, stream)
+                          : launch_wr_plain<MODE, VAR, 2, 3, 5, 1, 64>(base, off, delta, nkeys, out, stream);
+        default: return w4 ? launch_wr_plain<MODE, VAR, 2, 2, 3, 4, 64>(base, off, delta, nkeys, out, stream)
+                           : launch_wr_plain<MODE, VAR, 2, 2, 3, 1, 64>(base, off, delta, nkeys, out, stream);
+        }
+    }
     switch ((var >> 8) & 7) {
     case 1: return w4 ? launch_wr_plain<MODE, VAR, 4, 1, 2, 4>(base, off, delta, nkeys, out, stream)
                       : launch_wr_plain<MODE, VAR, 4, 1, 2, 1>(base, off, delta, nkeys, out, stream);
@@ -1621,13 +1730,13 @@ template <int MODE>
 hipError_t launch_wr_mode(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                           hipStream_t stream, int var)
 {
-    if constexpr (MODE == NC_GPUHASH_FNV1A_64) {
-        if (var & (2048 | 4096)) {
-            const int v = (var & 1) | ((var & 4096) ? 512 : 0);
+    if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_MD5) {
+        if (var & (2048 | 4096 | 8192 | 16384)) { /* bit 14: pinned look-ahead reads */
+            const int v = ((var & 4096) ? 512 : 0) | ((var & 16384) ? 1024 : 0);
             switch (v) {
-            case 1: return launch_wr_x<MODE, 1>(base, off, delta, nkeys, out, stream, var);
             case 512: return launch_wr_x<MODE, 512>(base, off, delta, nkeys, out, stream, var);
-            case 513: return launch_wr_x<MODE, 513>(base, off, delta, nkeys, out, stream, var);
+            case 1024: return launch_wr_x<MODE, 1024>(base, off, delta, nkeys, out, stream, var);
+            case 1536: return launch_wr_x<MODE, 1536>(base, off, delta, nkeys, out, stream, var);
             default: return launch_wr_x<MODE, 0>(base, off, delta, nkeys, out, stream, var);
             }
         }

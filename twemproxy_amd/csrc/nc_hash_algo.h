@@ -180,81 +180,101 @@ NC_HD uint32_t nc_jenkins_init(uint32_t len) { return 0xdeadbeefu + len + 13u; }
     (a) = nc_rotl((a), (s));                     \
     (a) += (b); } while (0)
 
+/* The 64 steps: (round function, a, b, c, d, message word, constant, shift). */
+#define NC_MD5_ROUNDS(S) \
+    S(NC_MD5_F, a, b, c, d, 0, 0xd76aa478u, 7) \
+    S(NC_MD5_F, d, a, b, c, 1, 0xe8c7b756u, 12) \
+    S(NC_MD5_F, c, d, a, b, 2, 0x242070dbu, 17) \
+    S(NC_MD5_F, b, c, d, a, 3, 0xc1bdceeeu, 22) \
+    S(NC_MD5_F, a, b, c, d, 4, 0xf57c0fafu, 7) \
+    S(NC_MD5_F, d, a, b, c, 5, 0x4787c62au, 12) \
+    S(NC_MD5_F, c, d, a, b, 6, 0xa8304613u, 17) \
+    S(NC_MD5_F, b, c, d, a, 7, 0xfd469501u, 22) \
+    S(NC_MD5_F, a, b, c, d, 8, 0x698098d8u, 7) \
+    S(NC_MD5_F, d, a, b, c, 9, 0x8b44f7afu, 12) \
+    S(NC_MD5_F, c, d, a, b, 10, 0xffff5bb1u, 17) \
+    S(NC_MD5_F, b, c, d, a, 11, 0x895cd7beu, 22) \
+    S(NC_MD5_F, a, b, c, d, 12, 0x6b901122u, 7) \
+    S(NC_MD5_F, d, a, b, c, 13, 0xfd987193u, 12) \
+    S(NC_MD5_F, c, d, a, b, 14, 0xa679438eu, 17) \
+    S(NC_MD5_F, b, c, d, a, 15, 0x49b40821u, 22) \
+    S(NC_MD5_G, a, b, c, d, 1, 0xf61e2562u, 5) \
+    S(NC_MD5_G, d, a, b, c, 6, 0xc040b340u, 9) \
+    S(NC_MD5_G, c, d, a, b, 11, 0x265e5a51u, 14) \
+    S(NC_MD5_G, b, c, d, a, 0, 0xe9b6c7aau, 20) \
+    S(NC_MD5_G, a, b, c, d, 5, 0xd62f105du, 5) \
+    S(NC_MD5_G, d, a, b, c, 10, 0x02441453u, 9) \
+    S(NC_MD5_G, c, d, a, b, 15, 0xd8a1e681u, 14) \
+    S(NC_MD5_G, b, c, d, a, 4, 0xe7d3fbc8u, 20) \
+    S(NC_MD5_G, a, b, c, d, 9, 0x21e1cde6u, 5) \
+    S(NC_MD5_G, d, a, b, c, 14, 0xc33707d6u, 9) \
+    S(NC_MD5_G, c, d, a, b, 3, 0xf4d50d87u, 14) \
+    S(NC_MD5_G, b, c, d, a, 8, 0x455a14edu, 20) \
+    S(NC_MD5_G, a, b, c, d, 13, 0xa9e3e905u, 5) \
+    S(NC_MD5_G, d, a, b, c, 2, 0xfcefa3f8u, 9) \
+    S(NC_MD5_G, c, d, a, b, 7, 0x676f02d9u, 14) \
+    S(NC_MD5_G, b, c, d, a, 12, 0x8d2a4c8au, 20) \
+    S(NC_MD5_H, a, b, c, d, 5, 0xfffa3942u, 4) \
+    S(NC_MD5_H, d, a, b, c, 8, 0x8771f681u, 11) \
+    S(NC_MD5_H, c, d, a, b, 11, 0x6d9d6122u, 16) \
+    S(NC_MD5_H, b, c, d, a, 14, 0xfde5380cu, 23) \
+    S(NC_MD5_H, a, b, c, d, 1, 0xa4beea44u, 4) \
+    S(NC_MD5_H, d, a, b, c, 4, 0x4bdecfa9u, 11) \
+    S(NC_MD5_H, c, d, a, b, 7, 0xf6bb4b60u, 16) \
+    S(NC_MD5_H, b, c, d, a, 10, 0xbebfbc70u, 23) \
+    S(NC_MD5_H, a, b, c, d, 13, 0x289b7ec6u, 4) \
+    S(NC_MD5_H, d, a, b, c, 0, 0xeaa127fau, 11) \
+    S(NC_MD5_H, c, d, a, b, 3, 0xd4ef3085u, 16) \
+    S(NC_MD5_H, b, c, d, a, 6, 0x04881d05u, 23) \
+    S(NC_MD5_H, a, b, c, d, 9, 0xd9d4d039u, 4) \
+    S(NC_MD5_H, d, a, b, c, 12, 0xe6db99e5u, 11) \
+    S(NC_MD5_H, c, d, a, b, 15, 0x1fa27cf8u, 16) \
+    S(NC_MD5_H, b, c, d, a, 2, 0xc4ac5665u, 23) \
+    S(NC_MD5_I, a, b, c, d, 0, 0xf4292244u, 6) \
+    S(NC_MD5_I, d, a, b, c, 7, 0x432aff97u, 10) \
+    S(NC_MD5_I, c, d, a, b, 14, 0xab9423a7u, 15) \
+    S(NC_MD5_I, b, c, d, a, 5, 0xfc93a039u, 21) \
+    S(NC_MD5_I, a, b, c, d, 12, 0x655b59c3u, 6) \
+    S(NC_MD5_I, d, a, b, c, 3, 0x8f0ccc92u, 10) \
+    S(NC_MD5_I, c, d, a, b, 10, 0xffeff47du, 15) \
+    S(NC_MD5_I, b, c, d, a, 1, 0x85845dd1u, 21) \
+    S(NC_MD5_I, a, b, c, d, 8, 0x6fa87e4fu, 6) \
+    S(NC_MD5_I, d, a, b, c, 15, 0xfe2ce6e0u, 10) \
+    S(NC_MD5_I, c, d, a, b, 6, 0xa3014314u, 15) \
+    S(NC_MD5_I, b, c, d, a, 13, 0x4e0811a1u, 21) \
+    S(NC_MD5_I, a, b, c, d, 4, 0xf7537e82u, 6) \
+    S(NC_MD5_I, d, a, b, c, 11, 0xbd3af235u, 10) \
+    S(NC_MD5_I, c, d, a, b, 2, 0x2ad7d2bbu, 15) \
+    S(NC_MD5_I, b, c, d, a, 9, 0xeb86d391u, 21)
+
+#define NC_MD5_S1(f, a, b, c, d, k, t, s) NC_MD5_STEP(f, a, b, c, d, w[k], t, s);
 NC_HD void nc_md5_block(uint32_t st[4], const uint32_t w[16])
 {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
-    NC_MD5_STEP(NC_MD5_F, a, b, c, d, w[0], 0xd76aa478u, 7);
-    NC_MD5_STEP(NC_MD5_F, d, a, b, c, w[1], 0xe8c7b756u, 12);
-    NC_MD5_STEP(NC_MD5_F, c, d, a, b, w[2], 0x242070dbu, 17);
-    NC_MD5_STEP(NC_MD5_F, b, c, d, a, w[3], 0xc1bdceeeu, 22);
-    NC_MD5_STEP(NC_MD5_F, a, b, c, d, w[4], 0xf57c0fafu, 7);
-    NC_MD5_STEP(NC_MD5_F, d, a, b, c, w[5], 0x4787c62au, 12);
-    NC_MD5_STEP(NC_MD5_F, c, d, a, b, w[6], 0xa8304613u, 17);
-    NC_MD5_STEP(NC_MD5_F, b, c, d, a, w[7], 0xfd469501u, 22);
-    NC_MD5_STEP(NC_MD5_F, a, b, c, d, w[8], 0x698098d8u, 7);
-    NC_MD5_STEP(NC_MD5_F, d, a, b, c, w[9], 0x8b44f7afu, 12);
-    NC_MD5_STEP(NC_MD5_F, c, d, a, b, w[10], 0xffff5bb1u, 17);
-    NC_MD5_STEP(NC_MD5_F, b, c, d, a, w[11], 0x895cd7beu, 22);
-    NC_MD5_STEP(NC_MD5_F, a, b, c, d, w[12], 0x6b901122u, 7);
-    NC_MD5_STEP(NC_MD5_F, d, a, b, c, w[13], 0xfd987193u, 12);
-    NC_MD5_STEP(NC_MD5_F, c, d, a, b, w[14], 0xa679438eu, 17);
-    NC_MD5_STEP(NC_MD5_F, b, c, d, a, w[15], 0x49b40821u, 22);
-
-    NC_MD5_STEP(NC_MD5_G, a, b, c, d, w[1], 0xf61e2562u, 5);
-    NC_MD5_STEP(NC_MD5_G, d, a, b, c, w[6], 0xc040b340u, 9);
-    NC_MD5_STEP(NC_MD5_G, c, d, a, b, w[11], 0x265e5a51u, 14);
-    NC_MD5_STEP(NC_MD5_G, b, c, d, a, w[0], 0xe9b6c7aau, 20);
-    NC_MD5_STEP(NC_MD5_G, a, b, c, d, w[5], 0xd62f105du, 5);
-    NC_MD5_STEP(NC_MD5_G, d, a, b, c, w[10], 0x02441453u, 9);
-    NC_MD5_STEP(NC_MD5_G, c, d, a, b, w[15], 0xd8a1e681u, 14);
-    NC_MD5_STEP(NC_MD5_G, b, c, d, a, w[4], 0xe7d3fbc8u, 20);
-    NC_MD5_STEP(NC_MD5_G, a, b, c, d, w[9], 0x21e1cde6u, 5);
-    NC_MD5_STEP(NC_MD5_G, d, a, b, c, w[14], 0xc33707d6u, 9);
-    NC_MD5_STEP(NC_MD5_G, c, d, a, b, w[3], 0xf4d50d87u, 14);
-    NC_MD5_STEP(NC_MD5_G, b, c, d, a, w[8], 0x455a14edu, 20);
-    NC_MD5_STEP(NC_MD5_G, a, b, c, d, w[13], 0xa9e3e905u, 5);
-    NC_MD5_STEP(NC_MD5_G, d, a, b, c, w[2], 0xfcefa3f8u, 9);
-    NC_MD5_STEP(NC_MD5_G, c, d, a, b, w[7], 0x676f02d9u, 14);
-    NC_MD5_STEP(NC_MD5_G, b, c, d, a, w[12], 0x8d2a4c8au, 20);
-
-    NC_MD5_STEP(NC_MD5_H, a, b, c, d, w[5], 0xfffa3942u, 4);
-    NC_MD5_STEP(NC_MD5_H, d, a, b, c, w[8], 0x8771f681u, 11);
-    NC_MD5_STEP(NC_MD5_H, c, d, a, b, w[11], 0x6d9d6122u, 16);
-    NC_MD5_STEP(NC_MD5_H, b, c, d, a, w[14], 0xfde5380cu, 23);
-    NC_MD5_STEP(NC_MD5_H, a, b, c, d, w[1], 0xa4beea44u, 4);
-    NC_MD5_STEP(NC_MD5_H, d, a, b, c, w[4], 0x4bdecfa9u, 11);
-    NC_MD5_STEP(NC_MD5_H, c, d, a, b, w[7], 0xf6bb4b60u, 16);
-    NC_MD5_STEP(NC_MD5_H, b, c, d, a, w[10], 0xbebfbc70u, 23);
-    NC_MD5_STEP(NC_MD5_H, a, b, c, d, w[13], 0x289b7ec6u, 4);
-    NC_MD5_STEP(NC_MD5_H, d, a, b, c, w[0], 0xeaa127fau, 11);
-    NC_MD5_STEP(NC_MD5_H, c, d, a, b, w[3], 0xd4ef3085u, 16);
-    NC_MD5_STEP(NC_MD5_H, b, c, d, a, w[6], 0x04881d05u, 23);
-    NC_MD5_STEP(NC_MD5_H, a, b, c, d, w[9], 0xd9d4d039u, 4);
-    NC_MD5_STEP(NC_MD5_H, d, a, b, c, w[12], 0xe6db99e5u, 11);
-    NC_MD5_STEP(NC_MD5_H, c, d, a, b, w[15], 0x1fa27cf8u, 16);
-    NC_MD5_STEP(NC_MD5_H, b, c, d, a, w[2], 0xc4ac5665u, 23);
-
-    NC_MD5_STEP(NC_MD5_I, a, b, c, d, w[0], 0xf4292244u, 6);
-    NC_MD5_STEP(NC_MD5_I, d, a, b, c, w[7], 0x432aff97u, 10);
-    NC_MD5_STEP(NC_MD5_I, c, d, a, b, w[14], 0xab9423a7u, 15);
-    NC_MD5_STEP(NC_MD5_I, b, c, d, a, w[5], 0xfc93a039u, 21);
-    NC_MD5_STEP(NC_MD5_I, a, b, c, d, w[12], 0x655b59c3u, 6);
-    NC_MD5_STEP(NC_MD5_I, d, a, b, c, w[3], 0x8f0ccc92u, 10);
-    NC_MD5_STEP(NC_MD5_I, c, d, a, b, w[10], 0xffeff47du, 15);
-    NC_MD5_STEP(NC_MD5_I, b, c, d, a, w[1], 0x85845dd1u, 21);
-    NC_MD5_STEP(NC_MD5_I, a, b, c, d, w[8], 0x6fa87e4fu, 6);
-    NC_MD5_STEP(NC_MD5_I, d, a, b, c, w[15], 0xfe2ce6e0u, 10);
-    NC_MD5_STEP(NC_MD5_I, c, d, a, b, w[6], 0xa3014314u, 15);
-    NC_MD5_STEP(NC_MD5_I, b, c, d, a, w[13], 0x4e0811a1u, 21);
-    NC_MD5_STEP(NC_MD5_I, a, b, c, d, w[4], 0xf7537e82u, 6);
-    NC_MD5_STEP(NC_MD5_I, d, a, b, c, w[11], 0xbd3af235u, 10);
-    NC_MD5_STEP(NC_MD5_I, c, d, a, b, w[2], 0x2ad7d2bbu, 15);
-    NC_MD5_STEP(NC_MD5_I, b, c, d, a, w[9], 0xeb86d391u, 21);
-
+    NC_MD5_ROUNDS(NC_MD5_S1)
     st[0] += a;
     st[1] += b;
     st[2] += c;
     st[3] += d;
+}
+
+/* Two independent blocks with their steps alternating, so the two
+ * dependency chains overlap on an in-order core (one lane, two keys). */
+#define NC_MD5_S2(f, a, b, c, d, k, t, s) \
+    NC_MD5_STEP(f, a##0, b##0, c##0, d##0, w0[k], t, s); NC_MD5_STEP(f, a##1, b##1, c##1, d##1, w1[k], t, s);
+NC_HD void nc_md5_block2(uint32_t s0[4], const uint32_t w0[16], uint32_t s1[4], const uint32_t w1[16])
+{
+    uint32_t a0 = s0[0], b0 = s0[1], c0 = s0[2], d0 = s0[3];
+    uint32_t a1 = s1[0], b1 = s1[1], c1 = s1[2], d1 = s1[3];
+    NC_MD5_ROUNDS(NC_MD5_S2)
+    s0[0] += a0;
+    s0[1] += b0;
+    s0[2] += c0;
+    s0[3] += d0;
+    s1[0] += a1;
+    s1[1] += b1;
+    s1[2] += c1;
+    s1[3] += d1;
 }
 
 #define NC_MD5_A0 0x67452301u
