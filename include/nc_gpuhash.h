@@ -93,14 +93,40 @@ const char *nc_gpuhash_mode_name(int mode);
 rstatus_t nc_gpuhash_batch_device(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
                                   uint64_t nkeys, uint32_t *d_out, void *stream);
 
+/* What the packer of a batch knows about it (all host-side facts, no device
+ * read): Σ key bytes = offsets[nkeys] - offsets[0], and the shortest and
+ * longest key. It selects the kernel pipeline; every choice
+ * gives identical outputs. Zero key_bytes (or a NULL shape) = unknown. */
+struct nc_gpuhash_shape {
+    uint64_t key_bytes;
+    uint32_t min_len;
+    uint32_t max_len;
+};
+
+/* nc_gpuhash_batch_device with the batch shape (NULL = unknown, the same as
+ * nc_gpuhash_batch_device). */
+rstatus_t nc_gpuhash_batch_device_shaped(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
+                                         uint64_t nkeys, uint32_t *d_out,
+                                         const struct nc_gpuhash_shape *shape, void *stream);
+
+/* The launch variant the auto policy picks for this mode and shape (the
+ * variant bits of nc_gpuhash_set_tuning; bit 16 = the plain workgroup
+ * pipeline); -1 with errno EINVAL for an invalid mode. */
+int nc_gpuhash_pick_variant(int mode, uint64_t nkeys, const struct nc_gpuhash_shape *shape);
+
 /* Same launch repeated `iters` times between two hipEvents recorded on
  * `stream`; blocks until done and stores the mean milliseconds per launch. */
 rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
                                  uint64_t nkeys, uint32_t *d_out, void *stream,
                                  int iters, float *avg_ms);
+rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
+                                        uint64_t nkeys, uint32_t *d_out,
+                                        const struct nc_gpuhash_shape *shape, void *stream,
+                                        int iters, float *avg_ms);
 
 /* Launch tuning (process-wide; for tests and benchmarks; every setting gives
- * identical outputs). grid_cap: maximum workgroups per launch (0 = persistent,
+ * identical outputs; variant 0 = the shape-driven auto policy, any other
+ * value is used as given). grid_cap: maximum workgroups per launch (0 = persistent,
  * one per resident slot; -1 = keep). sort: group a tile's keys by length
  * before hashing (1 on, 0 off, -1 keep). variant: kernel code variant bits
  * (bit 0: shift-add FNV-64 multiply; bits 1-2: L2 prefetch distance code,
@@ -109,7 +135,9 @@ rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, const uint64_t
  * for fixed 32-byte keys, fnv1a_64 unsorted only; bit 5: register-staged
  * pipeline, two tiles in flight; bit 6: default cache policy on the key,
  * offset and output streams instead of non-temporal, fnv1a_64 and md5 only;
- * -1 = keep). */
+ * bit 7: wave-ring pipeline, bits 8-10 its slab/look-ahead shape; bits 11-15:
+ * wave-ring experiments (fnv1a_64, md5, crc32); bit 16: the plain workgroup
+ * pipeline as an explicit choice; -1 = keep). */
 rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
 /* ---- 3b. host batches through a context (pinned staging, one stream per slot) ---- */

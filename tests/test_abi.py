@@ -128,3 +128,27 @@ def test_batched_path_fails_loudly_without_gpu():
         t.Context()
     rc = L.lib().nc_gpuhash_batch_device(99, None, None, 1, None, None)
     assert rc == L.NC_ERROR and ctypes.get_errno() == errno.EINVAL
+
+
+def test_auto_policy_choices():
+    """Shape-driven pipeline choice (host logic): the register-
+    staged workgroup pipeline when the shape is unknown or lengths vary, the
+    wave ring for fixed 20-40 B fnv-like keys and for long keys."""
+    WG, RS, RING5, RING4 = 1 << 16, 32, 128 | (3 << 8), 128
+    n = 1 << 26
+    assert t.pick_variant("fnv1a_64", n) == RS
+    assert t.pick_variant("fnv1a_64", n, (19 * n, 8, 64)) == RS  # C2 (Zipf)
+    assert t.pick_variant("fnv1a_64", n, (36 * n, 8, 64)) == RS  # uniform 8-64
+    for name in ("fnv1_64", "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur"):
+        assert t.pick_variant(name, n, (32 * n, 32, 32)) == RING5, name  # C3
+    for name in ("crc16", "crc32", "crc32a"):
+        assert t.pick_variant(name, n, (32 * n, 32, 32)) == WG, name
+    for name in ("one_at_a_time", "md5", "jenkins"):
+        assert t.pick_variant(name, n, (32 * n, 32, 32)) == RS, name
+    assert t.pick_variant("fnv1a_64", n, (8 * n, 8, 8)) == WG
+    assert t.pick_variant("crc32", n >> 3, (256 * (n >> 3), 256, 256)) == RING4  # C4
+    assert t.pick_variant("md5", n >> 3, (256 * (n >> 3), 256, 256)) == RING5
+    assert t.pick_variant("md5", n >> 3, (128 * (n >> 3), 128, 128)) == WG
+    assert t.pick_variant("hsieh", 1000, (100000, 100, 100)) == RING5
+    assert t.pick_variant("fnv1a_64", 0, (0, 0, 0)) == RS
+    assert L.lib().nc_gpuhash_pick_variant(12, n, None) == -1

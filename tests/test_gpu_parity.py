@@ -36,11 +36,11 @@ def gpu_hash(mode, keys_d, off_d):
     return out.cpu().numpy().view(np.uint32)
 
 
-@pytest.fixture(params=[(0, 1, 0), (0, 0, 0), (37, 1, 1), (0, 0, 3), (5, 1, 2), (0, 0, 4), (3, 1, 6),
+@pytest.fixture(params=[(0, 1, 0), (0, 0, 0), (0, 0, 65536), (37, 1, 1), (0, 0, 3), (5, 1, 2), (0, 0, 4), (3, 1, 6),
                         (0, 0, 32), (0, 1, 32), (11, 1, 33), (9, 0, 32), (0, 0, 64), (0, 1, 64),
                         (0, 0, 96), (7, 1, 96), (0, 0, 128), (37, 0, 129), (0, 0, 384), (5, 0, 640),
                         (0, 0, 896), (0, 0, 192), (0, 0, 2432 | 4096), (3, 0, 3968 | 4096 | 16384)],
-                ids=["persistent+sort", "persistent", "grid37+sort+shiftadd", "shiftadd+pf2",
+                ids=["persistent+sort", "auto", "workgroup", "grid37+sort+shiftadd", "shiftadd+pf2",
                      "grid5+sort+pf2", "pf3", "grid3+sort+pf4", "regstage", "regstage+sort",
                      "grid11+regstage+sort+shiftadd", "grid9+regstage", "cached", "cached+sort",
                      "regstage+cached", "grid7+regstage+cached+sort", "wavering", "grid37+wavering+shiftadd",
@@ -137,6 +137,29 @@ def test_long_keys_global_path(gpu, oracle, tuning, lo, hi, n):
         np.testing.assert_array_equal(gpu_hash(m, kd, od), oracle.batch(m, keys, off), err_msg=t.HASH_NAMES[m])
 
 
+@pytest.mark.parametrize("spec", [t.SynthSpec.fixed(21, 8), t.SynthSpec.fixed(22, 16), t.SynthSpec.fixed(23, 32),
+                                  t.SynthSpec.fixed(24, 40), t.SynthSpec.fixed(25, 64), t.SynthSpec.fixed(26, 128),
+                                  t.SynthSpec.fixed(27, 256), t.SynthSpec.zipf(28), t.SynthSpec.uniform(29, 8, 64),
+                                  t.SynthSpec.uniform(30, 60, 300), t.SynthSpec.uniform(31, 0, 3)],
+                         ids=lambda s: f"d{s.len_dist}_{s.len_a}_{s.len_b}")
+def test_auto_policy_by_shape(gpu, oracle, spec):
+    """Every pipeline the shape-driven policy can pick, against the oracle, with
+    ragged last tiles; the same keys without a shape agree too."""
+    for n in (4099, 70001):
+        keys, off = t.synth_host(spec, 5, n)
+        kd, od = to_dev(keys, off)
+        shape = t.shape_of(off)
+        for m in MODES:
+            want = oracle.batch(m, keys, off)
+            got = t.hash_batch_device(m, kd, od, shape=shape)
+            import torch
+
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want,
+                                          err_msg=f"{t.HASH_NAMES[m]} var {t.pick_variant(m, n, shape)}")
+            np.testing.assert_array_equal(gpu_hash(m, kd, od), want, err_msg=t.HASH_NAMES[m])
+
+
 def test_synth_device_matches_host(gpu):
     for spec in (t.SynthSpec.zipf(2), t.SynthSpec.fixed(3, 32), t.SynthSpec.uniform(6, 0, 600),
                  t.SynthSpec.zipf(5, charset=t.BYTES_PRINTABLE)):
@@ -159,7 +182,8 @@ def test_full_size_digests(gpu, digests, cfg):
     assert sha(od.cpu().numpy().astype(np.uint64)) == d["sha256_offsets"]
     out = torch.empty(d["nkeys"], dtype=torch.int32, device="cuda")
     for name, want in d["modes"].items():
-        t.hash_batch_device(name, kd, od, out)
+        # with the shape the generator knows: the auto policy's pipeline at full size
+        t.hash_batch_device(name, kd, od, out, shape=spec.shape(d["key_bytes"]))
         torch.cuda.synchronize()
         got = out.cpu().numpy().view(np.uint32)
         assert got[:8].tolist() == want["head"], f"{cfg} {name}"
@@ -178,7 +202,7 @@ def test_c4_shape_slices_are_independent(gpu, oracle):
     kd, od = t.synth_device(spec, 0, n)
     rng = np.random.default_rng(3)
     for name in ("md5", "crc32"):
-        full = t.hash_batch_device(name, kd, od)
+        full = t.hash_batch_device(name, kd, od, shape=spec.shape(256 * n))
         torch.cuda.synchronize()
         fh = full.cpu().numpy().view(np.uint32)
         for _ in range(4):

@@ -18,7 +18,7 @@ ASM = os.path.join(ROOT, "twemproxy_amd", "csrc", "build", "nc_gpuhash_kernels.s
 
 @pytest.fixture(scope="module")
 def asm_file():
-    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "twemproxy_amd", "csrc"), "asm"],
+    r = subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "twemproxy_amd", "csrc"), "asm"],
                        capture_output=True, text=True)
     if r.returncode != 0 or not os.path.exists(ASM):
         pytest.fail("could not generate kernel assembly: " + r.stderr[-2000:])

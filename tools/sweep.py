@@ -4,7 +4,8 @@
     python tools/sweep.py [--modes fnv1a_64,md5] [--configs C2,C3] [--rounds 3] [--iters 20]
                           [--variants 0:0:0,0:1:1]
 
-variant = grid_cap:sort:var (var bit 0 = shift-add FNV multiply). Prints one JSON line per (config, mode, variant) with
+variant = grid_cap:sort:var (var bit 0 = shift-add FNV multiply). Configs: C1..C5, F<len> (fixed),
+U<lo>-<hi> (uniform lengths). Prints one JSON line per (config, mode, variant) with
 the median / min kernel ms (hipEvents over `iters` launches) and the
 algorithmic HBM fraction (sum(len + 12) per launch / time / 8 TB/s).
 """
@@ -35,10 +36,20 @@ def main():
 
     variants = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",")]
     for cfg in args.configs.split(","):
-        spec = t.CONFIGS[cfg]["spec"]
-        n = min(args.nkeys, t.CONFIGS[cfg]["nkeys"])
+        if cfg in t.CONFIGS:
+            spec = t.CONFIGS[cfg]["spec"]
+            n = min(args.nkeys, t.CONFIGS[cfg]["nkeys"])
+        elif cfg.startswith("F"):  # F<len>: fixed-length keys, about 2 GiB of key bytes
+            ln = int(cfg[1:])
+            spec = t.SynthSpec.fixed(7, ln)
+            n = min(args.nkeys, (1 << 31) // ln)
+        else:  # U<lo>-<hi>: uniform lengths
+            lo, hi = (int(x) for x in cfg[1:].split("-"))
+            spec = t.SynthSpec.uniform(8, lo, hi)
+            n = min(args.nkeys, (1 << 32) // (lo + hi))
         keys, off = t.synth_device(spec, 0, n)
         kb = int(off[-1].item())
+        shape = spec.shape(kb)  # var 0 = the auto policy for this shape; 65536 = the workgroup pipeline
         out = torch.empty(n, dtype=torch.int32, device="cuda")
         rd = [t.probe_read_gbs(keys, args.iters) for _ in range(args.rounds)]
         rdn = [t.probe_read_gbs(keys, args.iters, nt=True) for _ in range(args.rounds)]
@@ -51,8 +62,8 @@ def main():
             for _ in range(args.rounds):
                 for v in variants:
                     L.lib().nc_gpuhash_set_tuning(v[0], v[1], v[2])
-                    t.hash_batch_device(mode, keys, off, out)
-                    res[v].append(t.time_batch_device(mode, keys, off, out, args.iters))
+                    t.hash_batch_device(mode, keys, off, out, shape=shape)
+                    res[v].append(t.time_batch_device(mode, keys, off, out, args.iters, shape=shape))
             for v in variants:
                 med = statistics.median(res[v])
                 alg = kb + 12.0 * n

@@ -26,7 +26,9 @@ from .hashkit import (
     md5_signature,
     mode_of,
     pack_keys,
+    pick_variant,
     probe_read_gbs,
+    shape_of,
     shard_bounds,
     synth_device,
     synth_host,
@@ -37,6 +39,6 @@ __all__ = [
     "LIB_PATH", "NC_EAGAIN", "NC_ENOMEM", "NC_ERROR", "NC_GPUHASH_PAD", "NC_OK", "NcError", "lib",
     "BYTES_FULL", "BYTES_PRINTABLE", "CONFIGS", "DIST_NAMES", "HASH_DEFAULT", "HASH_NAMES", "NMODES",
     "Context", "SynthSpec", "conf_set_hash", "device_count", "hash_batch_device", "hash_batch_host",
-    "hash_key", "hash_keys", "ketama_hash", "md5_signature", "mode_of", "pack_keys", "probe_read_gbs", "shard_bounds",
+    "hash_key", "hash_keys", "ketama_hash", "md5_signature", "mode_of", "pack_keys", "pick_variant", "probe_read_gbs", "shape_of", "shard_bounds",
     "synth_device", "synth_host", "time_batch_device",
 ]

@@ -36,6 +36,12 @@ class NcSynthSpec(ctypes.Structure):
     ]
 
 
+class NcShape(ctypes.Structure):
+    """struct nc_gpuhash_shape (include/nc_gpuhash.h): what the packer knows about a batch."""
+
+    _fields_ = [("key_bytes", ctypes.c_uint64), ("min_len", ctypes.c_uint32), ("max_len", ctypes.c_uint32)]
+
+
 class NcKeySpan(ctypes.Structure):
     """struct nc_keyspan — the shape of twemproxy's struct keypos (src/nc_message.h:232-235)."""
 
@@ -66,6 +72,17 @@ SIGNATURES = {
     "nc_gpuhash_batch_device": (
         ctypes.c_int,
         [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p],
+    ),
+    "nc_gpuhash_batch_device_shaped": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.POINTER(NcShape),
+         ctypes.c_void_p],
+    ),
+    "nc_gpuhash_pick_variant": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(NcShape)]),
+    "nc_gpuhash_time_device_shaped": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.POINTER(NcShape),
+         ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float)],
     ),
     "nc_gpuhash_time_device": (
         ctypes.c_int,

@@ -227,7 +227,7 @@ static struct nc_slot *slot_acquire(nc_gpuhash_ctx_t *ctx, int *idx)
 
 /* Enqueue H2D -> kernel -> D2H on the slot's stream; staging already packed. */
 static rstatus_t slot_launch(nc_gpuhash_ctx_t *ctx, struct nc_slot *s, int idx, int mode, uint32_t nkeys,
-                             uint32_t *out, int *ticket)
+                             const struct nc_gpuhash_shape *shape, uint32_t *out, int *ticket)
 {
     const uint64_t nbytes = s->h_off[nkeys];
     memset(s->h_keys + nbytes, 0, NC_GPUHASH_PAD);
@@ -235,7 +235,8 @@ static rstatus_t slot_launch(nc_gpuhash_ctx_t *ctx, struct nc_slot *s, int idx, 
     if (e == hipSuccess) e = hipMemcpyAsync(s->d_keys, s->h_keys, nbytes + NC_GPUHASH_PAD, hipMemcpyHostToDevice, s->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(s->d_off, s->h_off, ((size_t)nkeys + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s->stream);
     if (e != hipSuccess) return hip_fail(e);
-    if (nc_gpuhash_batch_device(mode, s->d_keys, s->d_off, nkeys, s->d_out, s->stream) != NC_OK) return NC_ERROR;
+    if (nc_gpuhash_batch_device_shaped(mode, s->d_keys, s->d_off, nkeys, s->d_out, shape, s->stream) != NC_OK)
+        return NC_ERROR;
     e = hipMemcpyAsync(s->h_out, s->d_out, (size_t)nkeys * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipEventRecord(s->done, s->stream);
     if (e != hipSuccess) return hip_fail(e);
@@ -267,10 +268,15 @@ rstatus_t nc_gpuhash_submit(nc_gpuhash_ctx_t *ctx, int mode, const uint8_t *keys
     }
     if (nbytes) memcpy(s->h_keys, keys + offsets[0], nbytes);
     const uint64_t base = offsets[0];
-    for (uint32_t i = 0; i <= nkeys; i++) {
-        s->h_off[i] = offsets[i] - base;
+    struct nc_gpuhash_shape shape = {nbytes, UINT32_MAX, 0};
+    s->h_off[0] = 0;
+    for (uint32_t i = 0; i < nkeys; i++) {
+        const uint64_t len = offsets[i + 1] - offsets[i];
+        if (len < shape.min_len) shape.min_len = (uint32_t)len;
+        if (len > shape.max_len) shape.max_len = len > UINT32_MAX ? UINT32_MAX : (uint32_t)len;
+        s->h_off[i + 1] = offsets[i + 1] - base;
     }
-    return slot_launch(ctx, s, idx, mode, nkeys, out, ticket);
+    return slot_launch(ctx, s, idx, mode, nkeys, &shape, out, ticket);
 }
 
 rstatus_t nc_gpuhash_submit_spans(nc_gpuhash_ctx_t *ctx, int mode, const struct nc_keyspan *spans,
@@ -292,6 +298,7 @@ rstatus_t nc_gpuhash_submit_spans(nc_gpuhash_ctx_t *ctx, int mode, const struct 
         return NC_EAGAIN;
     }
     uint64_t pos = 0;
+    struct nc_gpuhash_shape shape = {0, UINT32_MAX, 0};
     s->h_off[0] = 0;
     for (uint32_t i = 0; i < nkeys; i++) {
         const size_t n = (size_t)(spans[i].end - spans[i].start);
@@ -302,8 +309,11 @@ rstatus_t nc_gpuhash_submit_spans(nc_gpuhash_ctx_t *ctx, int mode, const struct 
         memcpy(s->h_keys + pos, spans[i].start, n);
         pos += n;
         s->h_off[i + 1] = pos;
+        if (n < shape.min_len) shape.min_len = (uint32_t)n;
+        if (n > shape.max_len) shape.max_len = (uint32_t)n;
     }
-    return slot_launch(ctx, s, idx, mode, nkeys, out, ticket);
+    shape.key_bytes = pos;
+    return slot_launch(ctx, s, idx, mode, nkeys, &shape, out, ticket);
 }
 
 static struct nc_slot *slot_of(nc_gpuhash_ctx_t *ctx, int ticket)

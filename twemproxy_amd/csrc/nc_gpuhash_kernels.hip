@@ -1520,15 +1520,40 @@ __global__ __launch_bounds__(256) void nc_dispatch_kernel(const uint32_t *__rest
     }
 }
 
-/* ---------------- launch layer ---------------- */
+} // namespace
 
-int g_grid_cap = -1; /* 0 = persistent: every resident workgroup slot once */
-int g_sort = -1;     /* 1 on, 0 off */
-int g_variant = 0;   /* bit 0: shift-add FNV multiply; bits 1-2: L2 prefetch distance code
-                        (0 off, 1..3 -> 2..4 tiles ahead); bit 3: diagnostic no-hash build
-                        (fnv1a_64, unsorted; outputs are not hashes); bit 4: diagnostic
-                        arithmetic offsets; bit 5: register-staged kernel; bit 6: default
-                        cache policy instead of nt (fnv1a_64, md5) -- include/nc_gpuhash.h */
+/* ---------------- launch layer ----------------
+ *
+ * This file is compiled once per hash mode (-DNC_TU_MODE=<mode id>: that
+ * mode's kernels and its nc_tu::entry<MODE>) and once without NC_TU_MODE (the
+ * C ABI, the policy and the process-wide tuning state), so the 12 code
+ * objects build in parallel. */
+namespace nc_tu {
+extern int g_grid_cap; /* 0 = persistent: every resident workgroup slot once */
+extern int g_sort;     /* 1 on, 0 off */
+extern int g_variant;  /* variant bits, include/nc_gpuhash.h (nc_gpuhash_set_tuning) */
+extern int g_num_cus[64];
+
+/* one launch of mode MODE: the wave ring when var bit 7 is set (offsets
+ * 16-byte aligned), else the workgroup pipeline */
+template <int MODE>
+hipError_t entry(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                 hipStream_t stream, bool sort, int var);
+} // namespace nc_tu
+
+namespace {
+using nc_tu::g_grid_cap;
+using nc_tu::g_num_cus;
+using nc_tu::g_sort;
+using nc_tu::g_variant;
+
+/* Auto-policy choices (variant bits): the workgroup pipeline (bit 16 only
+ * marks an explicit choice; it is stripped before launch), the register-staged
+ * workgroup pipeline, and the wave ring with 5 KiB / 4 KiB slab slots. */
+constexpr int kVarWorkgroup = 1 << 16;
+constexpr int kVarRegStaged = 32;
+constexpr int kVarRingP5 = 128 | (3 << 8);
+constexpr int kVarRingP4 = 128;
 
 int grid_cap()
 {
@@ -1548,8 +1573,6 @@ bool sort_enabled()
     }
     return g_sort == 1;
 }
-
-int g_num_cus[64];
 
 int num_cus()
 {
@@ -1684,6 +1707,18 @@ hipError_t launch_wr_x(const uint8_t *base, const uint64_t *off, uint64_t delta,
                        hipStream_t stream, int var)
 {
     const bool w4 = (var & 2048) != 0;
+    if (var & 32768) { /* long keys: 64-key tiles in 8-16 KiB slab slots */
+        switch ((var >> 8) & 7) {
+        case 1: return w4 ? launch_wr_plain<MODE, VAR, 16, 1, 2, 4, 64>(base, off, delta, nkeys, out, stream)
+                          : launch_wr_plain<MODE, VAR, 16, 1, 2, 1, 64>(base, off, delta, nkeys, out, stream);
+        case 2: return w4 ? launch_wr_plain<MODE, VAR, 12, 1, 2, 4, 64>(base, off, delta, nkeys, out, stream)
+                          : launch_wr_plain<MODE, VAR, 12, 1, 2, 1, 64>(base, off, delta, nkeys, out, stream);
+        case 3: return w4 ? launch_wr_plain<MODE, VAR, 8, 2, 3, 4, 64>(base, off, delta, nkeys, out, stream)
+                          : launch_wr_plain<MODE, VAR, 8, 2, 3, 1, 64>(base, off, delta, nkeys, out, stream);
+        default: return w4 ? launch_wr_plain<MODE, VAR, 8, 1, 2, 4, 64>(base, off, delta, nkeys, out, stream)
+                           : launch_wr_plain<MODE, VAR, 8, 1, 2, 1, 64>(base, off, delta, nkeys, out, stream);
+        }
+    }
     if (var & 8192) { /* 64-key tiles, one key per lane */
         switch ((var >> 8) & 7) {
         case 1: return w4 ? launch_wr_plain<MODE, VAR, 2, 1, 2, 4, 64>(base, off, delta, nkeys, out, stream)
@@ -1730,8 +1765,8 @@ template <int MODE>
 hipError_t launch_wr_mode(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                           hipStream_t stream, int var)
 {
-    if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_MD5) {
-        if (var & (2048 | 4096 | 8192 | 16384)) { /* bit 14: pinned look-ahead reads */
+    if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_MD5 || MODE == NC_GPUHASH_CRC32) {
+        if (var & (2048 | 4096 | 8192 | 16384 | 32768)) { /* bit 14: pinned look-ahead reads */
             const int v = ((var & 4096) ? 512 : 0) | ((var & 16384) ? 1024 : 0);
             switch (v) {
             case 512: return launch_wr_x<MODE, 512>(base, off, delta, nkeys, out, stream, var);
@@ -1752,39 +1787,66 @@ hipError_t launch_wr_mode(const uint8_t *base, const uint64_t *off, uint64_t del
     return launch_wr_hash<MODE, 0>(base, off, delta, nkeys, out, stream, var);
 }
 
+} // namespace
+
+#ifdef NC_TU_MODE
+template <int MODE>
+hipError_t nc_tu::entry(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                        hipStream_t stream, bool sort, int var)
+{
+    if ((var & 128) != 0) return launch_wr_mode<MODE>(base, off, delta, nkeys, out, stream, var);
+    return launch_mode<MODE>(base, off, delta, nkeys, out, stream, sort, var);
+}
+template hipError_t nc_tu::entry<NC_TU_MODE>(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *,
+                                             hipStream_t, bool, int);
+#else /* the C ABI */
+
+int nc_tu::g_grid_cap = -1;
+int nc_tu::g_sort = -1;
+int nc_tu::g_variant = 0;
+int nc_tu::g_num_cus[64];
+
+namespace {
+
+/* Kernel choice of the auto policy (g_variant == 0) from the batch shape,
+ * measured on MI355X over fixed 8-256 B, Zipf 8-64 B and uniform 8-64 B key
+ * sets (profiles/r01_policy_sweep.txt). Every choice gives
+ * identical outputs. */
+int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
+{
+    if (sh == nullptr || nkeys == 0 || sh->key_bytes == 0) return kVarRegStaged;
+    const uint64_t mean = sh->key_bytes / nkeys;
+    const bool fixed = sh->max_len >= sh->min_len && sh->max_len - sh->min_len <= 4u;
+    const bool crc = mode == NC_GPUHASH_CRC16 || mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A;
+    const bool fnv_like = mode == NC_GPUHASH_FNV1_64 || mode == NC_GPUHASH_FNV1A_64 || mode == NC_GPUHASH_FNV1_32 ||
+                          mode == NC_GPUHASH_FNV1A_32 || mode == NC_GPUHASH_HSIEH || mode == NC_GPUHASH_MURMUR;
+    if (mean >= 80u) { /* tiles overflow the workgroup slab: wave ring, deeper or wider slab slots */
+        if (mode == NC_GPUHASH_MD5) return mean >= 192u ? kVarRingP5 : kVarWorkgroup;
+        if (mode == NC_GPUHASH_ONE_AT_A_TIME || mode == NC_GPUHASH_HSIEH) return kVarRingP5;
+        return kVarRingP4;
+    }
+    if (fixed && mean >= 20u && mean <= 40u) {
+        if (fnv_like) return kVarRingP5;
+        return crc ? kVarWorkgroup : kVarRegStaged;
+    }
+    if (fixed && mean < 20u) return kVarWorkgroup;
+    return kVarRegStaged;
+}
+
 hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
-                  hipStream_t stream)
+                  hipStream_t stream, const nc_gpuhash_shape *shape)
 {
     const uintptr_t kp = reinterpret_cast<uintptr_t>(d_keys);
     const uint8_t *base = reinterpret_cast<const uint8_t *>(kp & ~(uintptr_t)15);
     const uint64_t delta = (uint64_t)(kp & 15u);
     const bool sort = sort_enabled();
+    int var = g_variant != 0 ? g_variant & ~kVarWorkgroup : pick_variant(mode, nkeys, shape) & ~kVarWorkgroup;
     /* the wave ring DMAs offsets 16 bytes per lane: it needs 16-byte aligned
      * offsets (any other alignment takes the workgroup pipeline) */
-    if ((g_variant & 128) != 0 && (reinterpret_cast<uintptr_t>(d_off) & 15u) == 0) {
-        switch (mode) {
-#define NC_WCASE(M) \
-    case M: return launch_wr_mode<M>(base, d_off, delta, nkeys, d_out, stream, g_variant);
-            NC_WCASE(NC_GPUHASH_ONE_AT_A_TIME)
-            NC_WCASE(NC_GPUHASH_MD5)
-            NC_WCASE(NC_GPUHASH_CRC16)
-            NC_WCASE(NC_GPUHASH_CRC32)
-            NC_WCASE(NC_GPUHASH_CRC32A)
-            NC_WCASE(NC_GPUHASH_FNV1_64)
-            NC_WCASE(NC_GPUHASH_FNV1A_64)
-            NC_WCASE(NC_GPUHASH_FNV1_32)
-            NC_WCASE(NC_GPUHASH_FNV1A_32)
-            NC_WCASE(NC_GPUHASH_HSIEH)
-            NC_WCASE(NC_GPUHASH_MURMUR)
-            NC_WCASE(NC_GPUHASH_JENKINS)
-#undef NC_WCASE
-        default:
-            return hipErrorInvalidValue;
-        }
-    }
+    if ((var & 128) != 0 && (reinterpret_cast<uintptr_t>(d_off) & 15u) != 0) var = g_variant != 0 ? 0 : 32;
     switch (mode) {
 #define NC_CASE(M) \
-    case M: return launch_mode<M>(base, d_off, delta, nkeys, d_out, stream, sort, g_variant);
+    case M: return nc_tu::entry<M>(base, d_off, delta, nkeys, d_out, stream, sort, var);
         NC_CASE(NC_GPUHASH_ONE_AT_A_TIME)
         NC_CASE(NC_GPUHASH_MD5)
         NC_CASE(NC_GPUHASH_CRC16)
@@ -1811,15 +1873,31 @@ rstatus_t fail(int err)
 
 } // namespace
 
-extern "C" rstatus_t nc_gpuhash_batch_device(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
-                                             uint64_t nkeys, uint32_t *d_out, void *stream)
+extern "C" rstatus_t nc_gpuhash_batch_device_shaped(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
+                                                    uint64_t nkeys, uint32_t *d_out,
+                                                    const struct nc_gpuhash_shape *shape, void *stream)
 {
     if (mode < 0 || mode >= NC_GPUHASH_NMODES) return fail(EINVAL);
     if (nkeys == 0) return NC_OK;
     if (d_keys == nullptr || d_offsets == nullptr || d_out == nullptr) return fail(EINVAL);
-    hipError_t err = launch(mode, d_keys, d_offsets, nkeys, d_out, reinterpret_cast<hipStream_t>(stream));
+    hipError_t err = launch(mode, d_keys, d_offsets, nkeys, d_out, reinterpret_cast<hipStream_t>(stream), shape);
     if (err != hipSuccess) return fail(err == hipErrorNoDevice ? ENODEV : EIO);
     return NC_OK;
+}
+
+extern "C" rstatus_t nc_gpuhash_batch_device(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
+                                             uint64_t nkeys, uint32_t *d_out, void *stream)
+{
+    return nc_gpuhash_batch_device_shaped(mode, d_keys, d_offsets, nkeys, d_out, nullptr, stream);
+}
+
+extern "C" int nc_gpuhash_pick_variant(int mode, uint64_t nkeys, const struct nc_gpuhash_shape *shape)
+{
+    if (mode < 0 || mode >= NC_GPUHASH_NMODES) {
+        errno = EINVAL;
+        return -1;
+    }
+    return pick_variant(mode, nkeys, shape);
 }
 
 extern "C" rstatus_t nc_gpuhash_set_tuning(int grid_cap_, int sort, int variant)
@@ -1834,6 +1912,14 @@ extern "C" rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, con
                                             uint64_t nkeys, uint32_t *d_out, void *stream, int iters,
                                             float *avg_ms)
 {
+    return nc_gpuhash_time_device_shaped(mode, d_keys, d_offsets, nkeys, d_out, nullptr, stream, iters, avg_ms);
+}
+
+extern "C" rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
+                                                   uint64_t nkeys, uint32_t *d_out,
+                                                   const struct nc_gpuhash_shape *shape, void *stream, int iters,
+                                                   float *avg_ms)
+{
     if (mode < 0 || mode >= NC_GPUHASH_NMODES || iters <= 0 || avg_ms == nullptr) return fail(EINVAL);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipEvent_t a, b;
@@ -1845,7 +1931,7 @@ extern "C" rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, con
     rstatus_t rc = NC_OK;
     (void)hipEventRecord(a, st);
     for (int i = 0; i < iters && rc == NC_OK; i++) {
-        rc = nc_gpuhash_batch_device(mode, d_keys, d_offsets, nkeys, d_out, stream);
+        rc = nc_gpuhash_batch_device_shaped(mode, d_keys, d_offsets, nkeys, d_out, shape, stream);
     }
     (void)hipEventRecord(b, st);
     if (hipEventSynchronize(b) != hipSuccess) rc = fail(EIO);
@@ -1856,3 +1942,5 @@ extern "C" rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, con
     (void)hipEventDestroy(b);
     return rc;
 }
+
+#endif /* NC_TU_MODE */

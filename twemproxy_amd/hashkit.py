@@ -107,12 +107,38 @@ def _stream_handle(stream) -> int | None:
     return stream.cuda_stream
 
 
-def hash_batch_device(hash_: int | str, keys, offsets, out=None, stream=None):
+def _shape_arg(shape):
+    """(key_bytes, min_len, max_len) -> pointer to struct nc_gpuhash_shape, or None."""
+    if shape is None:
+        return None
+    return ctypes.byref(L.NcShape(int(shape[0]), int(shape[1]), int(shape[2])))
+
+
+def shape_of(offsets: np.ndarray) -> tuple[int, int, int]:
+    """Batch shape (key_bytes, min_len, max_len) of a host offset CSR."""
+    off = np.asarray(offsets, dtype=np.uint64)
+    if off.size < 2:
+        return 0, 0, 0
+    lens = np.diff(off)
+    return int(off[-1] - off[0]), int(lens.min()), int(lens.max())
+
+
+def pick_variant(hash_: int | str, nkeys: int, shape=None) -> int:
+    """The launch variant the auto policy picks (nc_gpuhash_pick_variant)."""
+    v = L.lib().nc_gpuhash_pick_variant(mode_of(hash_), nkeys, _shape_arg(shape))
+    if v < 0:
+        raise L.NcError(ctypes.get_errno(), "nc_gpuhash_pick_variant")
+    return v
+
+
+def hash_batch_device(hash_: int | str, keys, offsets, out=None, stream=None, shape=None):
     """Device-resident batch on torch tensors.
 
     keys: uint8 CUDA tensor readable NC_GPUHASH_PAD bytes past offsets[-1];
     offsets: int64 CUDA tensor of n+1 non-decreasing offsets;
     out: int32 CUDA tensor of n (allocated if None; the bits are the u32 hash).
+    shape: optional (key_bytes, min_len, max_len) the packer knows, used only
+    to pick the kernel pipeline (nc_gpuhash_batch_device_shaped).
     Enqueued on `stream` (default: torch's current stream).
     """
     import torch
@@ -128,24 +154,24 @@ def hash_batch_device(hash_: int | str, keys, offsets, out=None, stream=None):
     if out is None:
         out = torch.empty(max(n, 0), dtype=torch.int32, device=keys.device)
     L.check(
-        L.lib().nc_gpuhash_batch_device(
-            mode, keys.data_ptr(), offsets.data_ptr(), n, out.data_ptr(), _stream_handle(stream)
+        L.lib().nc_gpuhash_batch_device_shaped(
+            mode, keys.data_ptr(), offsets.data_ptr(), n, out.data_ptr(), _shape_arg(shape), _stream_handle(stream)
         ),
-        "nc_gpuhash_batch_device",
+        "nc_gpuhash_batch_device_shaped",
     )
     return out
 
 
-def time_batch_device(hash_: int | str, keys, offsets, out, iters: int, stream=None) -> float:
+def time_batch_device(hash_: int | str, keys, offsets, out, iters: int, stream=None, shape=None) -> float:
     """Mean ms per launch over `iters` launches, timed by hipEvents on the launch stream."""
     mode = mode_of(hash_)
     ms = ctypes.c_float(0.0)
     L.check(
-        L.lib().nc_gpuhash_time_device(
+        L.lib().nc_gpuhash_time_device_shaped(
             mode, keys.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, out.data_ptr(),
-            _stream_handle(stream), iters, ctypes.byref(ms),
+            _shape_arg(shape), _stream_handle(stream), iters, ctypes.byref(ms),
         ),
-        "nc_gpuhash_time_device",
+        "nc_gpuhash_time_device_shaped",
     )
     return float(ms.value)
 
@@ -280,6 +306,17 @@ class SynthSpec:
 
     def c(self) -> L.NcSynthSpec:
         return L.NcSynthSpec(self.seed, self.len_dist, self.len_a, self.len_b, self.charset, self.zipf_s)
+
+    def len_range(self) -> tuple[int, int]:
+        """(shortest, longest) key length the generator can produce."""
+        if self.len_dist == SYNTH_ZIPF:
+            return self.len_a, self.len_a - 1 + self.len_b
+        return self.len_a, self.len_b
+
+    def shape(self, key_bytes: int) -> tuple[int, int, int]:
+        """Batch shape (key_bytes, min_len, max_len) for hash_batch_device(shape=...)."""
+        lo, hi = self.len_range()
+        return int(key_bytes), lo, hi
 
     @staticmethod
     def fixed(seed: int, length: int, charset: int = BYTES_FULL) -> "SynthSpec":
