@@ -109,6 +109,31 @@ rstatus_t nc_gpuhash_batch_device_shaped(int mode, const uint8_t *d_keys, const 
                                          uint64_t nkeys, uint32_t *d_out,
                                          const struct nc_gpuhash_shape *shape, void *stream);
 
+/* ---- 3a'. fused server_pool_idx on the device ----
+ * Replaces the per-key server_pool_idx (src/nc_server.c:647-700) for a batch:
+ * hash_tag trimming (:665-677), server_pool_hash's empty-key rule (:639-641),
+ * the pool's hash (mode), then ketama_dispatch (src/hashkit/nc_ketama.c:222-246)
+ * or modula_dispatch (src/hashkit/nc_modula.c:146-156) over the pool's
+ * continuum, which the caller copies to the device once per rebuild (it
+ * changes only in ketama_update / modula_update). d_out[i] = server index.
+ * dist: NC_GPUHASH_DIST_KETAMA or _MODULA (DIST_RANDOM is libc random(),
+ * src/hashkit/nc_random.c:136-146, nondeterministic: EINVAL). nserver ==
+ * array_n(&pool->server); 1 gives all zeros without hashing (:655-658).
+ * hash_tag: NULL (none) or the pool's two tag bytes. d_offsets must be 16-byte
+ * aligned (hipMalloc'd buffers are), else EINVAL. */
+#define NC_GPUHASH_DIST_KETAMA 0 /* DIST_CODEC order, src/hashkit/nc_hashkit.h:38-41 */
+#define NC_GPUHASH_DIST_MODULA 1
+/* struct continuum, src/nc_server.h:64-67 (same layout) */
+struct nc_gpuhash_continuum {
+    uint32_t index;
+    uint32_t value;
+};
+rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint8_t *d_keys,
+                                       const uint64_t *d_offsets, uint64_t nkeys,
+                                       const struct nc_gpuhash_continuum *d_continuum,
+                                       uint32_t ncontinuum, uint32_t nserver, const char *hash_tag,
+                                       uint32_t *d_out, void *stream);
+
 /* The launch variant the auto policy picks for this mode and shape (the
  * variant bits of nc_gpuhash_set_tuning; bit 16 = the plain workgroup
  * pipeline); -1 with errno EINVAL for an invalid mode. */

@@ -528,3 +528,39 @@ uint32_t oracle_modula_dispatch(const uint32_t *indices, uint32_t n, uint32_t ha
 {
     return indices[hash % n];
 }
+
+/*
+ * server_pool_idx (src/nc_server.c:647-700) over a CSR batch, every server
+ * live: nserver == 1 -> 0 (:655-658); hash_tag trimming (:665-677): the first
+ * tag[0], then the first tag[1] after it, and with at least one byte between
+ * them the key becomes those bytes; server_pool_hash's keylen 0 -> hash 0
+ * (:639-641); then ketama_dispatch or modula_dispatch (:680-688).
+ */
+int oracle_server_idx_batch(int mode, int dist, const uint32_t *values, const uint32_t *indices,
+                            uint32_t ncont, uint32_t nserver, const char *tag,
+                            const uint8_t *keys, const uint64_t *offsets, uint64_t nkeys, uint32_t *out)
+{
+    if (mode < 0 || mode >= ORACLE_NMODES || (dist != 0 && dist != 1) || nserver == 0) return -1;
+    for (uint64_t i = 0; i < nkeys; i++) {
+        const uint8_t *key = keys + offsets[i];
+        uint32_t keylen = (uint32_t)(offsets[i + 1] - offsets[i]);
+        if (nserver == 1) {
+            out[i] = 0;
+            continue;
+        }
+        if (tag != NULL) {
+            const uint8_t *s = memchr(key, (uint8_t)tag[0], keylen);
+            if (s != NULL) {
+                const uint8_t *e = memchr(s + 1, (uint8_t)tag[1], (size_t)(key + keylen - (s + 1)));
+                if (e != NULL && e - s > 1) {
+                    key = s + 1;
+                    keylen = (uint32_t)(e - key);
+                }
+            }
+        }
+        const uint32_t h = keylen == 0 ? 0u : oracle_hash(mode, key, keylen);
+        out[i] = dist == 0 ? oracle_ketama_dispatch(values, indices, ncont, h)
+                           : oracle_modula_dispatch(indices, ncont, h);
+    }
+    return 0;
+}

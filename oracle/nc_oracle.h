@@ -80,6 +80,12 @@ int oracle_modula_build(const uint32_t *weights, uint32_t nserver,
                         uint32_t *indices, uint32_t cap);
 uint32_t oracle_modula_dispatch(const uint32_t *indices, uint32_t n, uint32_t hash);
 
+/* server_pool_idx (src/nc_server.c:647-700) over a CSR batch: dist 0 ketama
+ * (values + indices), 1 modula (indices); tag NULL or 2 bytes. 0 or -1. */
+int oracle_server_idx_batch(int mode, int dist, const uint32_t *values, const uint32_t *indices,
+                            uint32_t ncont, uint32_t nserver, const char *tag,
+                            const uint8_t *keys, const uint64_t *offsets, uint64_t nkeys, uint32_t *out);
+
 #ifdef __cplusplus
 }
 #endif

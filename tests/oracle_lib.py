@@ -47,6 +47,10 @@ class Oracle:
                                             ctypes.c_uint32]
         lib.oracle_modula_dispatch.restype = ctypes.c_uint32
         lib.oracle_modula_dispatch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+        lib.oracle_server_idx_batch.restype = ctypes.c_int
+        lib.oracle_server_idx_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         self.lib = lib
 
     def hash(self, mode: int, key: bytes) -> int:
@@ -95,6 +99,20 @@ class Oracle:
 
     def modula_dispatch(self, idx: np.ndarray, h: int) -> int:
         return int(self.lib.oracle_modula_dispatch(idx.ctypes.data, idx.size, h))
+
+    def server_idx_batch(self, mode: int, dist: int, vals, idx, nserver: int, tag, keys: np.ndarray,
+                         offsets: np.ndarray) -> np.ndarray:
+        """server_pool_idx per key (src/nc_server.c:647-700); vals may be None for modula."""
+        idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        vals = idx if vals is None else np.ascontiguousarray(vals, dtype=np.uint32)
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = offsets.size - 1
+        out = np.empty(n, dtype=np.uint32)
+        rc = self.lib.oracle_server_idx_batch(mode, dist, vals.ctypes.data, idx.ctypes.data, idx.size, nserver, tag,
+                                              keys.ctypes.data, offsets.ctypes.data, n, out.ctypes.data)
+        assert rc == 0
+        return out
 
 
 class RefHashkit:

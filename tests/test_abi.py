@@ -152,3 +152,14 @@ def test_auto_policy_choices():
     assert t.pick_variant("hsieh", 1000, (100000, 100, 100)) == RING5
     assert t.pick_variant("fnv1a_64", 0, (0, 0, 0)) == RS
     assert L.lib().nc_gpuhash_pick_variant(12, n, None) == -1
+
+
+def test_server_idx_argument_errors():
+    """nc_gpuhash_server_idx_device argument checks (no device work): invalid
+    mode / DIST_RANDOM / zero servers are EINVAL; an empty batch is NC_OK."""
+    f = L.lib().nc_gpuhash_server_idx_device
+    for mode, dist, nserver in ((12, 0, 2), (-1, 0, 2), (6, 2, 2), (6, 3, 2), (6, 0, 0)):
+        ctypes.set_errno(0)
+        assert f(mode, dist, None, None, 5, None, 0, nserver, None, None, None) == L.NC_ERROR
+        assert ctypes.get_errno() == errno.EINVAL
+    assert f(6, 0, None, None, 0, None, 0, 2, None, None, None) == L.NC_OK

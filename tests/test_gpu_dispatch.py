@@ -1,0 +1,126 @@
+"""Fused server_pool_idx on the device through the C ABI
+(nc_gpuhash_server_idx_device), against the oracle's restatement of
+server_pool_idx (src/nc_server.c:647-700) over continua the compiled reference
+built (tests/golden/dist.json: ketama_update / modula_update output)."""
+import numpy as np
+import pytest
+
+import twemproxy_amd as t
+
+pytestmark = pytest.mark.gpu
+
+MODES = list(range(12))
+
+
+def to_dev(keys: np.ndarray, off: np.ndarray, shift: int = 0):
+    import torch
+
+    buf = torch.zeros(keys.size + shift + 64, dtype=torch.uint8, device="cuda")
+    buf[shift: shift + keys.size] = torch.from_numpy(keys).cuda()
+    return buf[shift:], torch.from_numpy(off.astype(np.int64)).cuda()
+
+
+def tagged_keyset(rng, n):
+    """Printable keys, some with {hash tags}: proper, empty {}, unclosed, reversed, repeated."""
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789:_-", dtype=np.uint8)
+    out = [b"", b"{}", b"{", b"}", b"}{", b"{a}", b"x{ab}y", b"{{a}}", b"a{b{c}d}e", b"{x}{y}", b"user:{42}:name"]
+    while len(out) < n:
+        body = rng.choice(alpha, size=int(rng.integers(0, 40))).tobytes()
+        r = rng.random()
+        if r < 0.4 and len(body) > 2:
+            i = int(rng.integers(0, len(body) - 1))
+            j = int(rng.integers(i, len(body)))
+            body = body[:i] + b"{" + body[i:j] + b"}" + body[j:]
+        elif r < 0.5:
+            body = body + b"{" + body[:3]
+        out.append(body)
+    return out
+
+
+def pools(dist_fixture):
+    for p in dist_fixture["pools"]:
+        yield p, len(p["names"])
+
+
+@pytest.mark.parametrize("tag", [None, b"{}", b"::"], ids=["notag", "braces", "colons"])
+def test_server_idx_matches_oracle(gpu, oracle, dist_fixture, tag):
+    import torch
+
+    rng = np.random.default_rng(17)
+    keyset = tagged_keyset(rng, 5000)
+    keys, off = t.pack_keys(keyset)
+    kd, od = to_dev(keys, off, shift=3)
+    for p, nserver in pools(dist_fixture):
+        kvals = np.array(p["ketama"]["values"], np.uint32)
+        kidx = np.array(p["ketama"]["indices"], np.uint32)
+        midx = np.array(p["modula"]["indices"], np.uint32)
+        conts = {"ketama": (t.continuum_device(kidx, kvals), kvals, kidx),
+                 "modula": (t.continuum_device(midx), None, midx)}
+        for dist, (cd, vals, idx) in conts.items():
+            for m in MODES:
+                got = t.server_idx_device(m, dist, kd, od, cd, nserver, hash_tag=tag)
+                torch.cuda.synchronize()
+                want = oracle.server_idx_batch(m, t.DIST_NAMES.index(dist), vals, idx, nserver, tag, keys, off)
+                np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want,
+                                              err_msg=f"{dist} {t.HASH_NAMES[m]} nserver={nserver} tag={tag}")
+
+
+def test_single_server_pool_is_all_zero(gpu):
+    import torch
+
+    keys, off = t.pack_keys([b"a", b"bb", b""] * 100)
+    kd, od = to_dev(keys, off)
+    cd = t.continuum_device(np.zeros(160, np.uint32), np.arange(160, dtype=np.uint32))
+    out = torch.full((300,), 7, dtype=torch.int32, device="cuda")
+    t.server_idx_device("fnv1a_64", "ketama", kd, od, cd, 1, out=out)
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tolist() == [0] * 300
+
+
+def test_random_dist_is_refused(gpu):
+    keys, off = t.pack_keys([b"a"])
+    kd, od = to_dev(keys, off)
+    cd = t.continuum_device(np.zeros(1, np.uint32))
+    with pytest.raises(t.NcError):
+        t.server_idx_device("fnv1a_64", "random", kd, od, cd, 2)
+
+
+def test_large_continuum_two_pass(gpu, oracle):
+    """A ketama continuum beyond the LDS budget (300 servers x 160 points x 8 B
+    = 375 KiB) takes the hash-then-dispatch pair of launches."""
+    import torch
+
+    names = [f"10.0.{i // 250}.{i % 250}:11211".encode() for i in range(300)]
+    vals, idx = oracle.ketama_build(names, [1] * len(names))
+    assert vals.size * 8 > 160 * 1024
+    keys, off = t.synth_host(t.SynthSpec.zipf(5, charset=t.BYTES_PRINTABLE), 0, 50000)
+    kd, od = to_dev(keys, off)
+    cd = t.continuum_device(idx, vals)
+    for m in (6, 1, 3):
+        got = t.server_idx_device(m, "ketama", kd, od, cd, len(names), hash_tag=b"{}")
+        torch.cuda.synchronize()
+        want = oracle.server_idx_batch(m, 0, vals, idx, len(names), b"{}", keys, off)
+        np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want)
+
+
+def test_server_idx_full_size_consistent_with_hash(gpu, dist_fixture):
+    """C2 shape at 2^24 keys: the fused kernel equals the hash kernel followed
+    by ketama_dispatch (a lower bound over the continuum values, wrapping)."""
+    import torch
+
+    p = dist_fixture["pools"][1]
+    kvals = np.array(p["ketama"]["values"], np.uint32)
+    kidx = np.array(p["ketama"]["indices"], np.uint32)
+    kd, od = t.synth_device(t.CONFIGS["C2"]["spec"], 0, 1 << 24)
+    cd = t.continuum_device(kidx, kvals)
+    got = t.server_idx_device("fnv1a_64", "ketama", kd, od, cd, len(p["names"]))
+    h = t.hash_batch_device("fnv1a_64", kd, od)
+    torch.cuda.synchronize()
+    hv = h.cpu().numpy().view(np.uint32)
+    pos = np.searchsorted(kvals, hv, side="left")
+    pos[pos == kvals.size] = 0
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), kidx[pos])
+    midx = np.array(p["modula"]["indices"], np.uint32)
+    got = t.server_idx_device("fnv1a_64", "modula", kd, od, t.continuum_device(midx), len(p["names"]))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), midx[hv % midx.size])

@@ -32,9 +32,10 @@ def main():
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     g, s, v = (int(x) for x in args.variant.split(":"))
     L.lib().nc_gpuhash_set_tuning(g, s, v)
+    shape = cfg["spec"].shape(int(off[-1].item()))  # as bench.py: the auto policy's pipeline
     for mode in args.mode.split(","):
         for _ in range(args.iters):
-            t.hash_batch_device(mode, keys, off, out)
+            t.hash_batch_device(mode, keys, off, out, shape=shape)
     torch.cuda.synchronize()
     print(f"{args.config} {args.mode} {args.variant} n={n} key_bytes={int(off[-1].item())}")
 

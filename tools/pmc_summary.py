@@ -20,10 +20,13 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    m = re.search(r"nc_hash_kernel<(\d+), (true|false), (\d+)>", name)
+    m = re.search(r"(nc_hash_kernel(?:_rs)?)<(\d+), (true|false), (\d+)>", name)
     if m:
-        return f"nc_hash_kernel<mode={m.group(1)},sort={m.group(2)},var={m.group(3)}>"
-    return name.split("(")[0][:80]
+        return f"{m.group(1)}<mode={m.group(2)},sort={m.group(3)},var={m.group(4)}>"
+    m = re.search(r"(nc_hash_kernel_wr)<([-\d, ]+)>", name)
+    if m:
+        return f"{m.group(1)}<{m.group(2)}>"
+    return name.replace("void (anonymous namespace)::", "").split("(")[0][:80]
 
 
 def counters(path):

@@ -1539,6 +1539,19 @@ extern int g_num_cus[64];
 template <int MODE>
 hipError_t entry(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                  hipStream_t stream, bool sort, int var);
+
+/* server_pool_idx of one launch: continuum {index, value} pairs in device
+ * memory, hash_tag (c0 | c1 << 8 | 1 << 16, or 0), kind 0 ketama / 1 modula */
+struct DistArgs {
+    const uint32_t *cont;
+    uint32_t ncont;
+    uint32_t tag;
+    int kind;
+};
+/* fused hash -> dispatch of mode MODE on the wave ring (offsets 16-byte aligned) */
+template <int MODE>
+hipError_t entry_dist(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                      hipStream_t stream, const DistArgs &d);
 } // namespace nc_tu
 
 namespace {
@@ -1799,6 +1812,39 @@ hipError_t nc_tu::entry(const uint8_t *base, const uint64_t *off, uint64_t delta
 }
 template hipError_t nc_tu::entry<NC_TU_MODE>(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *,
                                              hipStream_t, bool, int);
+
+/* The continuum is staged in LDS next to four waves' rings when it fits
+ * (ketama: 160 points per server, src/hashkit/nc_ketama.c:26-27, so up to
+ * ~100 servers); a larger one takes the hash-then-dispatch pair of launches,
+ * the second reading the continuum through L2. */
+template <int MODE>
+hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys,
+                             uint32_t *out, hipStream_t stream, const DistArgs &d)
+{
+    constexpr int P = 4, DS = 2, DO = 3, WPW = 4;
+    constexpr size_t kMaxLds = 160u * 1024u;
+    const WrDist wd{d.cont, d.ncont, d.tag};
+    const size_t fixed = wr_lds_fixed<MODE, kDistKetama, P, DS, DO, WPW>();
+    const size_t lds = fixed + 8u * (size_t)d.ncont;
+    if (lds <= kMaxLds) {
+        return d.kind == 0 ? launch_wr<MODE, 0, P, DS, DO, kDistKetama, WPW>(base, off, delta, nkeys, out, stream, wd, lds)
+                           : launch_wr<MODE, 0, P, DS, DO, kDistModula, WPW>(base, off, delta, nkeys, out, stream, wd, lds);
+    }
+    hipError_t e = launch_wr<MODE, 0, P, DS, DO, kDistPre, WPW>(base, off, delta, nkeys, out, stream, wd, fixed);
+    if (e != hipSuccess) return e;
+    uint64_t grid = (nkeys + 255u) / 256u;
+    const uint64_t cap = (uint64_t)num_cus() * 8u;
+    if (grid > cap) grid = cap;
+    if (d.kind == 0)
+        hipLaunchKernelGGL(nc_dispatch_kernel<kDistKetama>, dim3((unsigned)grid), dim3(256), 0, stream, d.cont, d.ncont,
+                           out, nkeys);
+    else
+        hipLaunchKernelGGL(nc_dispatch_kernel<kDistModula>, dim3((unsigned)grid), dim3(256), 0, stream, d.cont, d.ncont,
+                           out, nkeys);
+    return hipGetLastError();
+}
+template hipError_t nc_tu::entry_dist<NC_TU_MODE>(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *,
+                                                  hipStream_t, const DistArgs &);
 #else /* the C ABI */
 
 int nc_tu::g_grid_cap = -1;
@@ -1889,6 +1935,54 @@ extern "C" rstatus_t nc_gpuhash_batch_device(int mode, const uint8_t *d_keys, co
                                              uint64_t nkeys, uint32_t *d_out, void *stream)
 {
     return nc_gpuhash_batch_device_shaped(mode, d_keys, d_offsets, nkeys, d_out, nullptr, stream);
+}
+
+extern "C" rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint8_t *d_keys,
+                                                  const uint64_t *d_offsets, uint64_t nkeys,
+                                                  const struct nc_gpuhash_continuum *d_continuum,
+                                                  uint32_t ncontinuum, uint32_t nserver, const char *hash_tag,
+                                                  uint32_t *d_out, void *stream)
+{
+    if (mode < 0 || mode >= NC_GPUHASH_NMODES) return fail(EINVAL);
+    if (dist != NC_GPUHASH_DIST_KETAMA && dist != NC_GPUHASH_DIST_MODULA) return fail(EINVAL);
+    if (nserver == 0) return fail(EINVAL);
+    if (nkeys == 0) return NC_OK;
+    if (d_keys == nullptr || d_offsets == nullptr || d_out == nullptr) return fail(EINVAL);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (nserver == 1) { /* src/nc_server.c:655-658: no hashing, no dispatch */
+        const hipError_t e = hipMemsetAsync(d_out, 0, (size_t)nkeys * sizeof(uint32_t), st);
+        return e == hipSuccess ? NC_OK : fail(e == hipErrorNoDevice ? ENODEV : EIO);
+    }
+    if (d_continuum == nullptr || ncontinuum == 0) return fail(EINVAL);
+    if ((reinterpret_cast<uintptr_t>(d_offsets) & 15u) != 0) return fail(EINVAL);
+    const uintptr_t kp = reinterpret_cast<uintptr_t>(d_keys);
+    const uint8_t *base = reinterpret_cast<const uint8_t *>(kp & ~(uintptr_t)15);
+    const uint64_t delta = (uint64_t)(kp & 15u);
+    nc_tu::DistArgs d{reinterpret_cast<const uint32_t *>(d_continuum), ncontinuum, 0u, dist};
+    if (hash_tag != nullptr)
+        d.tag = (uint32_t)(uint8_t)hash_tag[0] | ((uint32_t)(uint8_t)hash_tag[1] << 8) | (1u << 16);
+    hipError_t e;
+    switch (mode) {
+#define NC_DCASE(M) \
+    case M: e = nc_tu::entry_dist<M>(base, d_offsets, delta, nkeys, d_out, st, d); break;
+        NC_DCASE(NC_GPUHASH_ONE_AT_A_TIME)
+        NC_DCASE(NC_GPUHASH_MD5)
+        NC_DCASE(NC_GPUHASH_CRC16)
+        NC_DCASE(NC_GPUHASH_CRC32)
+        NC_DCASE(NC_GPUHASH_CRC32A)
+        NC_DCASE(NC_GPUHASH_FNV1_64)
+        NC_DCASE(NC_GPUHASH_FNV1A_64)
+        NC_DCASE(NC_GPUHASH_FNV1_32)
+        NC_DCASE(NC_GPUHASH_FNV1A_32)
+        NC_DCASE(NC_GPUHASH_HSIEH)
+        NC_DCASE(NC_GPUHASH_MURMUR)
+        NC_DCASE(NC_GPUHASH_JENKINS)
+#undef NC_DCASE
+    default:
+        return fail(EINVAL);
+    }
+    if (e != hipSuccess) return fail(e == hipErrorNoDevice ? ENODEV : EIO);
+    return NC_OK;
 }
 
 extern "C" int nc_gpuhash_pick_variant(int mode, uint64_t nkeys, const struct nc_gpuhash_shape *shape)

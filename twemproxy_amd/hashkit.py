@@ -162,6 +162,42 @@ def hash_batch_device(hash_: int | str, keys, offsets, out=None, stream=None, sh
     return out
 
 
+def continuum_device(indices, values=None, device="cuda"):
+    """A pool's continuum (struct continuum {index, value}, src/nc_server.h:64-67)
+    as the int32 (n, 2) device tensor server_idx_device takes; modula
+    continua carry value 0 (src/hashkit/nc_modula.c:128-129)."""
+    import torch
+
+    idx = np.ascontiguousarray(indices, dtype=np.uint32)
+    val = np.zeros_like(idx) if values is None else np.ascontiguousarray(values, dtype=np.uint32)
+    pairs = np.stack([idx, val], axis=1).view(np.int32)
+    return torch.from_numpy(np.ascontiguousarray(pairs)).to(device)
+
+
+def server_idx_device(hash_: int | str, dist: int | str, keys, offsets, continuum, nserver: int,
+                      hash_tag: bytes | None = None, out=None, stream=None):
+    """Fused server_pool_idx (src/nc_server.c:647-700) for a device-resident
+    batch: hash_tag trimming, the pool's hash, then ketama/modula dispatch over
+    `continuum` (continuum_device()). Returns the int32 server index per key."""
+    import torch
+
+    mode = mode_of(hash_)
+    d = DIST_NAMES.index(dist) if isinstance(dist, str) else int(dist)
+    n = offsets.numel() - 1
+    if hash_tag is not None and len(hash_tag) != 2:
+        raise ValueError("hash_tag is two bytes (conf_set_hash_tag)")
+    if out is None:
+        out = torch.empty(max(n, 0), dtype=torch.int32, device=keys.device)
+    L.check(
+        L.lib().nc_gpuhash_server_idx_device(
+            mode, d, keys.data_ptr(), offsets.data_ptr(), n, continuum.data_ptr(), continuum.shape[0], nserver,
+            hash_tag, out.data_ptr(), _stream_handle(stream),
+        ),
+        "nc_gpuhash_server_idx_device",
+    )
+    return out
+
+
 def time_batch_device(hash_: int | str, keys, offsets, out, iters: int, stream=None, shape=None) -> float:
     """Mean ms per launch over `iters` launches, timed by hipEvents on the launch stream."""
     mode = mode_of(hash_)
