@@ -269,7 +269,8 @@ def main():
         cont = t.continuum_device(cidx, cvals, device=dev)
         sidx = max(3, args.steps // 4)
         wd, kdd = timed_steps(t, torch, None, None, None, None, sidx, 1, dist_on, launch=lambda stream=None:
-                              t.server_idx_device("fnv1a_64", "ketama", keys, off, cont, 8, out=out, stream=stream))
+                              t.server_idx_device("fnv1a_64", "ketama", keys, off, cont, 8, out=out, stream=stream,
+                                                                shape=shape))
         wd = max_over_ranks(torch, wd, dist_on)
         res["server_idx_ketama"] = {
             "workload": "C2 keys, fnv1a_64 + ketama_dispatch, 8 servers x 160 points (LDS-staged continuum)",

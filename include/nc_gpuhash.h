@@ -119,8 +119,9 @@ rstatus_t nc_gpuhash_batch_device_shaped(int mode, const uint8_t *d_keys, const 
  * dist: NC_GPUHASH_DIST_KETAMA or _MODULA (DIST_RANDOM is libc random(),
  * src/hashkit/nc_random.c:136-146, nondeterministic: EINVAL). nserver ==
  * array_n(&pool->server); 1 gives all zeros without hashing (:655-658).
- * hash_tag: NULL (none) or the pool's two tag bytes. d_offsets must be 16-byte
- * aligned (hipMalloc'd buffers are), else EINVAL. */
+ * hash_tag: NULL (none) or the pool's two tag bytes. shape: NULL or the
+ * batch shape (it picks the slab size, as for nc_gpuhash_batch_device_shaped).
+ * d_offsets must be 16-byte aligned (hipMalloc'd buffers are), else EINVAL. */
 #define NC_GPUHASH_DIST_KETAMA 0 /* DIST_CODEC order, src/hashkit/nc_hashkit.h:38-41 */
 #define NC_GPUHASH_DIST_MODULA 1
 /* struct continuum, src/nc_server.h:64-67 (same layout) */
@@ -132,7 +133,8 @@ rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint8_t *d_keys
                                        const uint64_t *d_offsets, uint64_t nkeys,
                                        const struct nc_gpuhash_continuum *d_continuum,
                                        uint32_t ncontinuum, uint32_t nserver, const char *hash_tag,
-                                       uint32_t *d_out, void *stream);
+                                       const struct nc_gpuhash_shape *shape, uint32_t *d_out,
+                                       void *stream);
 
 /* The launch variant the auto policy picks for this mode and shape (the
  * variant bits of nc_gpuhash_set_tuning; bit 16 = the plain workgroup

@@ -160,6 +160,6 @@ def test_server_idx_argument_errors():
     f = L.lib().nc_gpuhash_server_idx_device
     for mode, dist, nserver in ((12, 0, 2), (-1, 0, 2), (6, 2, 2), (6, 3, 2), (6, 0, 0)):
         ctypes.set_errno(0)
-        assert f(mode, dist, None, None, 5, None, 0, nserver, None, None, None) == L.NC_ERROR
+        assert f(mode, dist, None, None, 5, None, 0, nserver, None, None, None, None) == L.NC_ERROR
         assert ctypes.get_errno() == errno.EINVAL
-    assert f(6, 0, None, None, 0, None, 0, 2, None, None, None) == L.NC_OK
+    assert f(6, 0, None, None, 0, None, 0, 2, None, None, None, None) == L.NC_OK

@@ -42,14 +42,17 @@ def pools(dist_fixture):
         yield p, len(p["names"])
 
 
+@pytest.mark.parametrize("wide", [False, True], ids=["narrow", "wide"])
 @pytest.mark.parametrize("tag", [None, b"{}", b"::"], ids=["notag", "braces", "colons"])
-def test_server_idx_matches_oracle(gpu, oracle, dist_fixture, tag):
+def test_server_idx_matches_oracle(gpu, oracle, dist_fixture, tag, wide):
     import torch
 
     rng = np.random.default_rng(17)
     keyset = tagged_keyset(rng, 5000)
     keys, off = t.pack_keys(keyset)
     kd, od = to_dev(keys, off, shift=3)
+    # the shape only picks the ring's slab size: claim 21 B/key for the wide one
+    shape = (21 * (off.size - 1), 0, 64) if wide else None
     for p, nserver in pools(dist_fixture):
         kvals = np.array(p["ketama"]["values"], np.uint32)
         kidx = np.array(p["ketama"]["indices"], np.uint32)
@@ -58,7 +61,7 @@ def test_server_idx_matches_oracle(gpu, oracle, dist_fixture, tag):
                  "modula": (t.continuum_device(midx), None, midx)}
         for dist, (cd, vals, idx) in conts.items():
             for m in MODES:
-                got = t.server_idx_device(m, dist, kd, od, cd, nserver, hash_tag=tag)
+                got = t.server_idx_device(m, dist, kd, od, cd, nserver, hash_tag=tag, shape=shape)
                 torch.cuda.synchronize()
                 want = oracle.server_idx_batch(m, t.DIST_NAMES.index(dist), vals, idx, nserver, tag, keys, off)
                 np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want,
@@ -96,8 +99,8 @@ def test_large_continuum_two_pass(gpu, oracle):
     keys, off = t.synth_host(t.SynthSpec.zipf(5, charset=t.BYTES_PRINTABLE), 0, 50000)
     kd, od = to_dev(keys, off)
     cd = t.continuum_device(idx, vals)
-    for m in (6, 1, 3):
-        got = t.server_idx_device(m, "ketama", kd, od, cd, len(names), hash_tag=b"{}")
+    for m, shape in ((6, None), (1, t.shape_of(off)), (3, (30 * 50000, 0, 64))):
+        got = t.server_idx_device(m, "ketama", kd, od, cd, len(names), hash_tag=b"{}", shape=shape)
         torch.cuda.synchronize()
         want = oracle.server_idx_batch(m, 0, vals, idx, len(names), b"{}", keys, off)
         np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want)

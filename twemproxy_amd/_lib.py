@@ -81,7 +81,8 @@ SIGNATURES = {
     "nc_gpuhash_server_idx_device": (
         ctypes.c_int,
         [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
-         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p],
+         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.POINTER(NcShape), ctypes.c_void_p,
+         ctypes.c_void_p],
     ),
     "nc_gpuhash_pick_variant": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(NcShape)]),
     "nc_gpuhash_time_device_shaped": (

@@ -1309,6 +1309,44 @@ __device__ __forceinline__ uint32_t ketama_find(const uint32_t *c, uint32_t n, u
     return c[2u * (lo == n ? 0u : lo)];
 }
 
+/* ketama_find narrowed by a 256-bucket index over the top hash byte:
+ * bkt[b] = first point with value >= b << 24 (bkt[256] = n), so the answer
+ * for h lies in [bkt[h >> 24], bkt[(h >> 24) + 1]] and the search takes
+ * ~log2(n / 256) + 1 steps instead of log2(n) */
+__device__ __forceinline__ uint32_t ketama_find_bkt(const uint32_t *c, const uint32_t *bkt, uint32_t n, uint32_t h)
+{
+    const uint32_t b = h >> 24;
+    uint32_t lo = bkt[b], len = bkt[b + 1u] - lo;
+    while (len > 0u) {
+        const uint32_t half = len >> 1;
+        if (c[2u * (lo + half) + 1u] < h) {
+            lo += half + 1u;
+            len -= half + 1u;
+        } else {
+            len = half;
+        }
+    }
+    return c[2u * (lo == n ? 0u : lo)];
+}
+
+/* lower bound of v over the continuum values (no wrap) */
+__device__ __forceinline__ uint32_t cont_lower_bound(const uint32_t *c, uint32_t n, uint32_t v)
+{
+    uint32_t lo = 0, len = n;
+    while (len > 0u) {
+        const uint32_t half = len >> 1;
+        if (c[2u * (lo + half) + 1u] < v) {
+            lo += half + 1u;
+            len -= half + 1u;
+        } else {
+            len = half;
+        }
+    }
+    return lo;
+}
+
+constexpr uint32_t kBktBytes = 4u * 260u; /* u32[257] bucket index after an LDS-staged ketama continuum */
+
 template <int MODE, int VAR, int DIST, class Src>
 __device__ __forceinline__ uint32_t key_value(const Src &src, typename Src::pos_t p, uint32_t len,
                                               const uint32_t *tab, const WrDist &dist, const uint32_t *cont)
@@ -1321,7 +1359,7 @@ __device__ __forceinline__ uint32_t key_value(const Src &src, typename Src::pos_
         if (dist.tag != 0u) tag_trim(src, p, len, dist.tag & 0xffu, (dist.tag >> 8) & 0xffu);
         uint32_t h = 0u; /* server_pool_hash: keylen 0 hashes to 0 (src/nc_server.c:639-641) */
         if (len != 0u) h = hash_key<MODE, VAR>(src, p, len, tab);
-        if constexpr (DIST == kDistKetama) return ketama_find(cont, dist.ncont, h);
+        if constexpr (DIST == kDistKetama) return ketama_find_bkt(cont, cont + 2u * dist.ncont, dist.ncont, h);
         else if constexpr (DIST == kDistModula) return cont[2u * (h % dist.ncont)]; /* nc_modula.c:153 */
         else return h;
     }
@@ -1362,7 +1400,13 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
     if constexpr (DIST == kDistKetama || DIST == kDistModula) {
         for (uint32_t i = t; i < 2u * dist.ncont; i += 64u * WPW) cont[i] = dist.cont[i];
     }
-    if constexpr (WPW > 1) __syncthreads();
+    if constexpr (DIST == kDistKetama) {
+        __syncthreads();
+        uint32_t *bkt = cont + 2u * dist.ncont;
+        for (uint32_t j = t; j <= 256u; j += 64u * WPW)
+            bkt[j] = j == 256u ? dist.ncont : cont_lower_bound(cont, dist.ncont, j << 24);
+    }
+    if constexpr (WPW > 1 || DIST == kDistKetama) __syncthreads();
 
     const uint64_t W = (uint64_t)gridDim.x * WPW;
     const uint64_t tile0 = (uint64_t)blockIdx.x * WPW + wave;
@@ -1547,6 +1591,7 @@ struct DistArgs {
     uint32_t ncont;
     uint32_t tag;
     int kind;
+    bool wide; /* 5 KiB slab slots two tiles ahead (keys of 20+ B) instead of 3 KiB one ahead */
 };
 /* fused hash -> dispatch of mode MODE on the wave ring (offsets 16-byte aligned) */
 template <int MODE>
@@ -1817,15 +1862,17 @@ template hipError_t nc_tu::entry<NC_TU_MODE>(const uint8_t *, const uint64_t *, 
  * (ketama: 160 points per server, src/hashkit/nc_ketama.c:26-27, so up to
  * ~100 servers); a larger one takes the hash-then-dispatch pair of launches,
  * the second reading the continuum through L2. */
-template <int MODE>
-hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys,
-                             uint32_t *out, hipStream_t stream, const DistArgs &d)
+namespace {
+/* server_pool_idx on ring shape <P, DS, DO>, four waves per workgroup */
+template <int MODE, int P, int DS, int DO>
+hipError_t dist_launch(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                       hipStream_t stream, const nc_tu::DistArgs &d)
 {
-    constexpr int P = 4, DS = 2, DO = 3, WPW = 4;
+    constexpr int WPW = 4;
     constexpr size_t kMaxLds = 160u * 1024u;
     const WrDist wd{d.cont, d.ncont, d.tag};
     const size_t fixed = wr_lds_fixed<MODE, kDistKetama, P, DS, DO, WPW>();
-    const size_t lds = fixed + 8u * (size_t)d.ncont;
+    const size_t lds = fixed + 8u * (size_t)d.ncont + (d.kind == 0 ? kBktBytes : 0u);
     if (lds <= kMaxLds) {
         return d.kind == 0 ? launch_wr<MODE, 0, P, DS, DO, kDistKetama, WPW>(base, off, delta, nkeys, out, stream, wd, lds)
                            : launch_wr<MODE, 0, P, DS, DO, kDistModula, WPW>(base, off, delta, nkeys, out, stream, wd, lds);
@@ -1842,6 +1889,15 @@ hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t 
         hipLaunchKernelGGL(nc_dispatch_kernel<kDistModula>, dim3((unsigned)grid), dim3(256), 0, stream, d.cont, d.ncont,
                            out, nkeys);
     return hipGetLastError();
+}
+} // namespace
+
+template <int MODE>
+hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys,
+                             uint32_t *out, hipStream_t stream, const DistArgs &d)
+{
+    return d.wide ? dist_launch<MODE, 5, 2, 3>(base, off, delta, nkeys, out, stream, d)
+                  : dist_launch<MODE, 3, 1, 2>(base, off, delta, nkeys, out, stream, d);
 }
 template hipError_t nc_tu::entry_dist<NC_TU_MODE>(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *,
                                                   hipStream_t, const DistArgs &);
@@ -1941,7 +1997,8 @@ extern "C" rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint
                                                   const uint64_t *d_offsets, uint64_t nkeys,
                                                   const struct nc_gpuhash_continuum *d_continuum,
                                                   uint32_t ncontinuum, uint32_t nserver, const char *hash_tag,
-                                                  uint32_t *d_out, void *stream)
+                                                  const struct nc_gpuhash_shape *shape, uint32_t *d_out,
+                                                  void *stream)
 {
     if (mode < 0 || mode >= NC_GPUHASH_NMODES) return fail(EINVAL);
     if (dist != NC_GPUHASH_DIST_KETAMA && dist != NC_GPUHASH_DIST_MODULA) return fail(EINVAL);
@@ -1958,7 +2015,8 @@ extern "C" rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint
     const uintptr_t kp = reinterpret_cast<uintptr_t>(d_keys);
     const uint8_t *base = reinterpret_cast<const uint8_t *>(kp & ~(uintptr_t)15);
     const uint64_t delta = (uint64_t)(kp & 15u);
-    nc_tu::DistArgs d{reinterpret_cast<const uint32_t *>(d_continuum), ncontinuum, 0u, dist};
+    const bool wide = shape != nullptr && shape->key_bytes > 20u * nkeys;
+    nc_tu::DistArgs d{reinterpret_cast<const uint32_t *>(d_continuum), ncontinuum, 0u, dist, wide};
     if (hash_tag != nullptr)
         d.tag = (uint32_t)(uint8_t)hash_tag[0] | ((uint32_t)(uint8_t)hash_tag[1] << 8) | (1u << 16);
     hipError_t e;

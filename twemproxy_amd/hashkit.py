@@ -175,7 +175,7 @@ def continuum_device(indices, values=None, device="cuda"):
 
 
 def server_idx_device(hash_: int | str, dist: int | str, keys, offsets, continuum, nserver: int,
-                      hash_tag: bytes | None = None, out=None, stream=None):
+                      hash_tag: bytes | None = None, out=None, stream=None, shape=None):
     """Fused server_pool_idx (src/nc_server.c:647-700) for a device-resident
     batch: hash_tag trimming, the pool's hash, then ketama/modula dispatch over
     `continuum` (continuum_device()). Returns the int32 server index per key."""
@@ -191,7 +191,7 @@ def server_idx_device(hash_: int | str, dist: int | str, keys, offsets, continuu
     L.check(
         L.lib().nc_gpuhash_server_idx_device(
             mode, d, keys.data_ptr(), offsets.data_ptr(), n, continuum.data_ptr(), continuum.shape[0], nserver,
-            hash_tag, out.data_ptr(), _stream_handle(stream),
+            hash_tag, _shape_arg(shape), out.data_ptr(), _stream_handle(stream),
         ),
         "nc_gpuhash_server_idx_device",
     )
