@@ -136,6 +136,20 @@ rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint8_t *d_keys
                                        const struct nc_gpuhash_shape *shape, uint32_t *d_out,
                                        void *stream);
 
+/* ketama_update (src/hashkit/nc_ketama.c:58-219) building the continuum
+ * straight into device memory for nc_gpuhash_server_idx_device: servers with
+ * live[s] == 0 are skipped as ejected (NULL = all live); points per server
+ * from the weights in the reference's float arithmetic (:159-160); 4 points
+ * per "<name>-<i>" md5 digest (:169-181, ketama_hash :31-41); sorted by value,
+ * ties in build order (:197-198). Writes *ncontinuum points (<= 160 x live
+ * servers for equal weights) to d_continuum; NC_ENOMEM if more than cap. A
+ * zero weight is EINVAL (the reference asserts weight > 0, :100). Blocks until
+ * the build is done (a cold path: once per rebuild). */
+rstatus_t nc_gpuhash_ketama_build_device(const char *const *names, const uint32_t *name_lens,
+                                         const uint32_t *weights, const uint8_t *live, uint32_t nserver,
+                                         struct nc_gpuhash_continuum *d_continuum, uint32_t cap,
+                                         uint32_t *ncontinuum, void *stream);
+
 /* The launch variant the auto policy picks for this mode and shape (the
  * variant bits of nc_gpuhash_set_tuning; bit 16 = the plain workgroup
  * pipeline); -1 with errno EINVAL for an invalid mode. */

@@ -452,23 +452,35 @@ int oracle_ketama_build(const char *const *names, const uint32_t *name_lens,
                         const uint32_t *weights, uint32_t nserver,
                         uint32_t *values, uint32_t *indices, uint32_t cap)
 {
-    uint32_t total = 0;
+    return oracle_ketama_build_live(names, name_lens, weights, NULL, nserver, values, indices, cap);
+}
+
+/* live[s] == 0: server s is ejected (auto_eject_hosts with next_retry > now,
+ * :80-102): no points, not in the total weight or the live count. */
+int oracle_ketama_build_live(const char *const *names, const uint32_t *name_lens,
+                             const uint32_t *weights, const uint8_t *live, uint32_t nserver,
+                             uint32_t *values, uint32_t *indices, uint32_t cap)
+{
+    uint32_t total = 0, nlive = 0;
     for (uint32_t s = 0; s < nserver; s++) {
         if (weights[s] == 0) return -1;
+        if (live != NULL && !live[s]) continue;
         total += weights[s];
+        nlive++;
     }
-    if (nserver == 0) return 0;
-    /* upper bound on points: each server gets <= 160*nserver points */
-    size_t maxpts = (size_t)nserver * 160u * nserver + 4;
+    if (nlive == 0) return 0;
+    /* upper bound on points: each server gets <= 160*nlive points */
+    size_t maxpts = (size_t)nlive * 160u * nlive + 4;
     struct o_point *pts = malloc(maxpts * sizeof(*pts));
     if (pts == NULL) return -1;
     uint32_t np = 0;
     for (uint32_t s = 0; s < nserver; s++) {
+        if (live != NULL && !live[s]) continue;
         /* pointer_per_server: float arithmetic as written at :159-160. */
         float pct = (float)weights[s] / (float)total;
         float t = pct * 160.0f;
         t = t / 4.0f;
-        t = t * (float)nserver;
+        t = t * (float)nlive;
         uint32_t pps = (uint32_t)(floorf((float)((double)t + 0.0000000001)) * 4.0f);
         for (uint32_t pi = 1; pi <= pps / 4; pi++) {
             char host[273];

@@ -72,6 +72,9 @@ double oracle_time_batch(int mode, const uint8_t *keys, const uint64_t *offsets,
 int oracle_ketama_build(const char *const *names, const uint32_t *name_lens,
                         const uint32_t *weights, uint32_t nserver,
                         uint32_t *values, uint32_t *indices, uint32_t cap);
+int oracle_ketama_build_live(const char *const *names, const uint32_t *name_lens,
+                             const uint32_t *weights, const uint8_t *live, uint32_t nserver,
+                             uint32_t *values, uint32_t *indices, uint32_t cap);
 uint32_t oracle_ketama_dispatch(const uint32_t *values, const uint32_t *indices,
                                 uint32_t n, uint32_t hash);
 /* modula_update (src/hashkit/nc_modula.c:34-143, all live): one point per

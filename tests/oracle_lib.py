@@ -40,6 +40,10 @@ class Oracle:
         lib.oracle_ketama_build.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint32),
                                             ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_uint32]
+        lib.oracle_ketama_build_live.restype = ctypes.c_int
+        lib.oracle_ketama_build_live.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint32),
+                                                 ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p, ctypes.c_uint32,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
         lib.oracle_ketama_dispatch.restype = ctypes.c_uint32
         lib.oracle_ketama_dispatch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
         lib.oracle_modula_build.restype = ctypes.c_int
@@ -76,13 +80,16 @@ class Oracle:
         return float(self.lib.oracle_time_batch(mode, keys.ctypes.data, offsets.ctypes.data, n,
                                                 out.ctypes.data, threads, reps))
 
-    def ketama_build(self, names: list[bytes], weights: list[int]) -> tuple[np.ndarray, np.ndarray]:
+    def ketama_build(self, names: list[bytes], weights: list[int], live=None) -> tuple[np.ndarray, np.ndarray]:
         n = len(names)
         cap = 160 * n * n + 16
         vals = np.zeros(cap, dtype=np.uint32)
         idx = np.zeros(cap, dtype=np.uint32)
-        cnt = self.lib.oracle_ketama_build((ctypes.c_char_p * n)(*names), (ctypes.c_uint32 * n)(*map(len, names)),
-                                           (ctypes.c_uint32 * n)(*weights), n, vals.ctypes.data, idx.ctypes.data, cap)
+        lv = None if live is None else (ctypes.c_uint8 * n)(*[1 if x else 0 for x in live])
+        cnt = self.lib.oracle_ketama_build_live((ctypes.c_char_p * n)(*names),
+                                                (ctypes.c_uint32 * n)(*map(len, names)),
+                                                (ctypes.c_uint32 * n)(*weights), lv, n, vals.ctypes.data,
+                                                idx.ctypes.data, cap)
         assert cnt >= 0
         return vals[:cnt], idx[:cnt]
 

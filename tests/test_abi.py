@@ -163,3 +163,20 @@ def test_server_idx_argument_errors():
         assert f(mode, dist, None, None, 5, None, 0, nserver, None, None, None, None) == L.NC_ERROR
         assert ctypes.get_errno() == errno.EINVAL
     assert f(6, 0, None, None, 0, None, 0, 2, None, None, None, None) == L.NC_OK
+
+
+def test_ketama_build_argument_errors():
+    """nc_gpuhash_ketama_build_device host-side checks (no device work)."""
+    f = L.lib().nc_gpuhash_ketama_build_device
+    names = (ctypes.c_char_p * 2)(b"a:1", b"b:2")
+    lens = (ctypes.c_uint32 * 2)(3, 3)
+    cnt = ctypes.c_uint32(7)
+    ctypes.set_errno(0)
+    assert f(names, lens, (ctypes.c_uint32 * 2)(1, 0), None, 2, None, 0, ctypes.byref(cnt), None) == L.NC_ERROR
+    assert ctypes.get_errno() == errno.EINVAL
+    # every server ejected: an empty continuum, as "no live servers" (nc_ketama.c:111-116)
+    dead = (ctypes.c_uint8 * 2)(0, 0)
+    assert f(names, lens, (ctypes.c_uint32 * 2)(1, 1), dead, 2, None, 0, ctypes.byref(cnt), None) == L.NC_OK
+    assert cnt.value == 0
+    # more points than cap: NC_ENOMEM before any device work
+    assert f(names, lens, (ctypes.c_uint32 * 2)(1, 1), None, 2, None, 10, ctypes.byref(cnt), None) == L.NC_ENOMEM

@@ -127,3 +127,48 @@ def test_server_idx_full_size_consistent_with_hash(gpu, dist_fixture):
     got = t.server_idx_device("fnv1a_64", "modula", kd, od, t.continuum_device(midx), len(p["names"]))
     torch.cuda.synchronize()
     np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), midx[hv % midx.size])
+
+
+def test_ketama_build_matches_reference(gpu, dist_fixture):
+    """ketama_update on the device reproduces the continua the compiled
+    reference built (values and indices, in order)."""
+    for p in dist_fixture["pools"]:
+        names = [n.encode() for n in p["names"]]
+        cont = t.ketama_build_device(names, p["weights"]).cpu().numpy().view(np.uint32)
+        assert cont[:, 1].tolist() == p["ketama"]["values"], p["names"][:2]
+        assert cont[:, 0].tolist() == p["ketama"]["indices"], p["names"][:2]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_ketama_build_weights_and_ejection(gpu, oracle, seed):
+    """Random weights, long and odd names, ejected servers: against the
+    oracle's restatement of ketama_update (parity with the reference pinned
+    for all-live pools by the test above)."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(2, 40))
+    names = [(b"h" * int(rng.integers(1, 300)) if i % 7 == 3 else f"10.1.{i}.{seed}:1121{i % 10}".encode())
+             for i in range(n)]
+    weights = [int(w) for w in rng.integers(1, 9, size=n)]
+    live = [bool(x) for x in rng.random(n) > 0.25]
+    live[0] = True
+    for lv in (None, live):
+        vals, idx = oracle.ketama_build(names, weights, lv)
+        cont = t.ketama_build_device(names, weights, lv).cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(cont[:, 1], vals)
+        np.testing.assert_array_equal(cont[:, 0], idx)
+
+
+def test_device_continuum_end_to_end(gpu, oracle):
+    """Continuum built on the device, then the fused server_pool_idx over it."""
+    import torch
+
+    names = [f"cache-{i}.example:11211".encode() for i in range(12)]
+    weights = [1, 2, 1, 3, 1, 1, 2, 1, 1, 1, 4, 1]
+    cd = t.ketama_build_device(names, weights)
+    vals, idx = oracle.ketama_build(names, weights)
+    keys, off = t.synth_host(t.SynthSpec.zipf(5, charset=t.BYTES_PRINTABLE), 0, 30000)
+    kd, od = to_dev(keys, off)
+    got = t.server_idx_device("md5", "ketama", kd, od, cd, len(names), hash_tag=b"{}")
+    torch.cuda.synchronize()
+    want = oracle.server_idx_batch(1, 0, vals, idx, len(names), b"{}", keys, off)
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want)

@@ -84,6 +84,12 @@ SIGNATURES = {
          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.POINTER(NcShape), ctypes.c_void_p,
          ctypes.c_void_p],
     ),
+    "nc_gpuhash_ketama_build_device": (
+        ctypes.c_int,
+        [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+         ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+         ctypes.c_void_p],
+    ),
     "nc_gpuhash_pick_variant": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(NcShape)]),
     "nc_gpuhash_time_device_shaped": (
         ctypes.c_int,

@@ -174,6 +174,30 @@ def continuum_device(indices, values=None, device="cuda"):
     return torch.from_numpy(np.ascontiguousarray(pairs)).to(device)
 
 
+def ketama_build_device(names: Sequence[bytes], weights: Sequence[int], live: Sequence[bool] | None = None,
+                        device="cuda", stream=None):
+    """ketama_update (src/hashkit/nc_ketama.c:58-219) on the device: the pool's
+    continuum as the int32 (n, 2) {index, value} tensor server_idx_device takes."""
+    import torch
+
+    n = len(names)
+    if live is not None and len(live) != n:
+        raise ValueError("live must have one flag per server")
+    nlive = n if live is None else int(sum(bool(x) for x in live))
+    cap = 160 * max(nlive, 1) + 16  # sum of floor(pct * 40 * nlive) * 4 <= 160 * nlive
+    cont = torch.empty((cap, 2), dtype=torch.int32, device=device)
+    lv = None if live is None else (ctypes.c_uint8 * n)(*[1 if x else 0 for x in live])
+    cnt = ctypes.c_uint32(0)
+    L.check(
+        L.lib().nc_gpuhash_ketama_build_device(
+            (ctypes.c_char_p * n)(*names), (ctypes.c_uint32 * n)(*[len(x) for x in names]),
+            (ctypes.c_uint32 * n)(*weights), lv, n, cont.data_ptr(), cap, ctypes.byref(cnt), _stream_handle(stream),
+        ),
+        "nc_gpuhash_ketama_build_device",
+    )
+    return cont[: cnt.value].clone()
+
+
 def server_idx_device(hash_: int | str, dist: int | str, keys, offsets, continuum, nserver: int,
                       hash_tag: bytes | None = None, out=None, stream=None, shape=None):
     """Fused server_pool_idx (src/nc_server.c:647-700) for a device-resident
