@@ -197,6 +197,13 @@ nc_gpuhash_ctx_t *nc_gpuhash_ctx_create(int device, uint64_t max_keys, uint64_t 
                                         int nslots);
 void nc_gpuhash_ctx_destroy(nc_gpuhash_ctx_t *ctx);
 
+/* Batches with at most max_key_bytes key bytes run zero-copy: the kernel
+ * reads the keys from the slot's mapped pinned staging across PCIe and writes
+ * the hashes back the same way, so no H2D/D2H copy is enqueued (one launch
+ * instead of three operations). 0 = always copy. The default is 1 MiB
+ * (environment NC_GPUHASH_ZERO_COPY=<bytes> overrides it at ctx_create). */
+rstatus_t nc_gpuhash_ctx_set_zero_copy(nc_gpuhash_ctx_t *ctx, uint64_t max_key_bytes);
+
 /* Pack a CSR batch into a free slot's pinned staging, enqueue H2D, kernel and
  * D2H, and return a ticket without blocking. NC_EAGAIN if every slot is busy,
  * NC_ENOMEM if the batch exceeds the context's limits. The caller may reuse

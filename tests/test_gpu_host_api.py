@@ -82,3 +82,16 @@ def test_context_limits(gpu):
             ctx.submit("md5", k, o)
         with pytest.raises(ValueError):
             ctx.submit("sha1", k, o)
+
+
+@pytest.mark.parametrize("zc", [1 << 14, 1 << 40])
+def test_context_zero_copy(gpu, oracle, zc):
+    """Zero-copy batches (kernel over mapped pinned staging) and copied ones
+    mixed in one context, every mode, ragged sizes, spans."""
+    with t.Context(max_keys=20000, max_key_bytes=1 << 20, nslots=3, zero_copy_bytes=zc) as ctx:
+        for i, n in enumerate((1, 255, 798, 3000, 20000)):
+            k, o = t.synth_host(t.SynthSpec.zipf(40 + i, charset=t.BYTES_PRINTABLE), 0, n)
+            for m in range(12):
+                tk, out = ctx.submit(m, k, o)
+                ctx.wait(tk)
+                np.testing.assert_array_equal(out, oracle.batch(m, k, o), err_msg=f"n={n} mode={m}")

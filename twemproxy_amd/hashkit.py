@@ -273,7 +273,8 @@ def hash_keys(hash_: int | str, keys: Sequence[bytes]) -> list[int]:
 class Context:
     """nc_gpuhash_ctx: pinned, multi-slot asynchronous host batches."""
 
-    def __init__(self, device: int = 0, max_keys: int = 65536, max_key_bytes: int = 1 << 22, nslots: int = 2):
+    def __init__(self, device: int = 0, max_keys: int = 65536, max_key_bytes: int = 1 << 22, nslots: int = 2,
+                 zero_copy_bytes: int | None = None):
         self._lib = L.lib()
         handle = self._lib.nc_gpuhash_ctx_create(device, max_keys, max_key_bytes, nslots)
         if not handle:
@@ -281,6 +282,12 @@ class Context:
             raise L.NcError(err, "nc_gpuhash_ctx_create failed")
         self._h = handle
         self._keep: dict[int, tuple] = {}
+        if zero_copy_bytes is not None:  # None: the library default (1 MiB)
+            self.set_zero_copy(zero_copy_bytes)
+
+    def set_zero_copy(self, max_key_bytes: int) -> None:
+        """Batches up to max_key_bytes skip the H2D/D2H copies (nc_gpuhash_ctx_set_zero_copy)."""
+        L.check(self._lib.nc_gpuhash_ctx_set_zero_copy(self._h, max_key_bytes), "nc_gpuhash_ctx_set_zero_copy")
 
     def close(self) -> None:
         if self._h:
