@@ -170,15 +170,17 @@ rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const u
  * value is used as given). grid_cap: maximum workgroups per launch (0 = persistent,
  * one per resident slot; -1 = keep). sort: group a tile's keys by length
  * before hashing (1 on, 0 off, -1 keep). variant: kernel code variant bits
- * (bit 0: shift-add FNV-64 multiply; bits 1-2: L2 prefetch distance code,
- * 0 off, 1..3 = 2..4 tiles ahead; bit 3: DIAGNOSTIC no-hash build, fnv1a_64
- * unsorted only, outputs are NOT hashes; bit 4: DIAGNOSTIC arithmetic offsets
+ * (bit 0: shift-add FNV-64 multiply; bit 3: DIAGNOSTIC no-hash build,
+ * fnv1a_64 unsorted only, outputs are NOT hashes, with bits 1-2 its L2
+ * prefetch distance code (0 off, 1..3 = 2..4 tiles ahead); bit 4: DIAGNOSTIC arithmetic offsets
  * for fixed 32-byte keys, fnv1a_64 unsorted only; bit 5: register-staged
  * pipeline, two tiles in flight; bit 6: default cache policy on the key,
  * offset and output streams instead of non-temporal, fnv1a_64 and md5 only;
- * bit 7: wave-ring pipeline, bits 8-10 its slab/look-ahead shape; bits 11-15:
- * wave-ring experiments (fnv1a_64, md5, crc32); bit 16: the plain workgroup
- * pipeline as an explicit choice; -1 = keep). */
+ * bit 7: wave-ring pipeline, bits 8-10 its slab/look-ahead shape; bits 11-13:
+ * wave-ring experiments (fnv1a_64, md5: 4 waves per workgroup, pair-
+ * interleaved keys, 64-key tiles); bit 16: the plain workgroup
+ * pipeline as an explicit choice; bit 17: length-grouped tiles, as sort = 1;
+ * -1 = keep). */
 rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
 /* ---- 3b. host batches through a context (pinned staging, one stream per slot) ---- */

@@ -137,14 +137,20 @@ def test_auto_policy_choices():
     WG, RS, RING5, RING4 = 1 << 16, 32, 128 | (3 << 8), 128
     n = 1 << 26
     assert t.pick_variant("fnv1a_64", n) == RS
+    assert t.pick_variant("md5", n) == RS  # unknown shape
     assert t.pick_variant("fnv1a_64", n, (19 * n, 8, 64)) == RS  # C2 (Zipf)
     assert t.pick_variant("fnv1a_64", n, (36 * n, 8, 64)) == RS  # uniform 8-64
+    SORTED = 1 << 17
+    assert t.pick_variant("md5", n, (19 * n, 8, 64)) == WG | SORTED
+    assert t.pick_variant("md5", n, (36 * n, 8, 64)) == RS | SORTED
+    assert t.pick_variant("crc32", n, (19 * n, 8, 64)) == WG | SORTED
+    assert t.pick_variant("crc32a", n, (36 * n, 8, 64)) == RS
     for name in ("fnv1_64", "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == RING5, name  # C3
     for name in ("crc16", "crc32", "crc32a"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == WG, name
     for name in ("one_at_a_time", "md5", "jenkins"):
-        assert t.pick_variant(name, n, (32 * n, 32, 32)) == RS, name
+        assert t.pick_variant(name, n, (32 * n, 32, 32)) == RS, name  # fixed: no grouping
     assert t.pick_variant("fnv1a_64", n, (8 * n, 8, 8)) == WG
     assert t.pick_variant("crc32", n >> 3, (256 * (n >> 3), 256, 256)) == RING4  # C4
     assert t.pick_variant("md5", n >> 3, (256 * (n >> 3), 256, 256)) == RING5

@@ -36,16 +36,17 @@ def gpu_hash(mode, keys_d, off_d):
     return out.cpu().numpy().view(np.uint32)
 
 
-@pytest.fixture(params=[(0, 1, 0), (0, 0, 0), (0, 0, 65536), (37, 1, 1), (0, 0, 3), (5, 1, 2), (0, 0, 4), (3, 1, 6),
-                        (0, 0, 32), (0, 1, 32), (11, 1, 33), (9, 0, 32), (0, 0, 64), (0, 1, 64),
+@pytest.fixture(params=[(0, 1, 0), (0, 0, 0), (0, 0, 65536), (37, 1, 1), (0, 0, 1), (5, 1, 65536),
+                        (0, 0, 1 << 17), (0, 0, 32), (0, 1, 32), (11, 1, 33), (9, 0, 32), (0, 0, 64), (0, 1, 64),
                         (0, 0, 96), (7, 1, 96), (0, 0, 128), (37, 0, 129), (0, 0, 384), (5, 0, 640),
-                        (0, 0, 896), (0, 0, 192), (0, 0, 2432 | 4096), (3, 0, 3968 | 4096 | 16384)],
-                ids=["persistent+sort", "auto", "workgroup", "grid37+sort+shiftadd", "shiftadd+pf2",
-                     "grid5+sort+pf2", "pf3", "grid3+sort+pf4", "regstage", "regstage+sort",
-                     "grid11+regstage+sort+shiftadd", "grid9+regstage", "cached", "cached+sort",
-                     "regstage+cached", "grid7+regstage+cached+sort", "wavering", "grid37+wavering+shiftadd",
-                     "wavering_4_1_2", "grid5+wavering_4_3_5", "wavering_5_2_3", "wavering+cached",
-                     "wavering_w4_pair", "grid3+wavering_3_1_2_w4_pair_pin"])
+                        (0, 0, 896), (0, 0, 192), (0, 0, 2432 | 4096), (3, 0, 3968 | 4096), (0, 0, 2176),
+                        (0, 0, 10624)],
+                ids=["persistent+sort", "auto", "workgroup", "grid37+sort+shiftadd", "shiftadd", "grid5+sort",
+                     "sorted_bit", "regstage", "regstage+sort", "grid11+regstage+sort+shiftadd", "grid9+regstage",
+                     "cached", "cached+sort", "regstage+cached", "grid7+regstage+cached+sort", "wavering",
+                     "grid37+wavering+shiftadd", "wavering_4_1_2", "grid5+wavering_4_3_5", "wavering_5_2_3",
+                     "wavering+cached", "wavering_w4_pair", "grid3+wavering_3_1_2_w4_pair", "wavering_w4",
+                     "wavering_t64_w4"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)
@@ -227,8 +228,8 @@ def test_sort_and_grid_variants_agree_full_size(gpu):
 
     kd, od = t.synth_device(t.CONFIGS["C2"]["spec"], 0, 1 << 24)
     ref = None
-    for grid, sort, var in ((0, 1, 0), (0, 0, 0), (2048, 1, 1), (4096, 0, 1), (1, 0, 0), (0, 0, 2), (0, 1, 2),
-                            (3, 1, 3), (0, 0, 4), (7, 0, 6), (0, 0, 32), (0, 1, 32), (5, 1, 33), (13, 1, 32), (1024, 0, 32),
+    for grid, sort, var in ((0, 1, 0), (0, 0, 0), (2048, 1, 1), (4096, 0, 1), (1, 0, 0), (0, 0, 65536),
+                            (0, 1, 65536), (3, 1, 1), (0, 0, 1 << 17), (7, 0, 2176), (0, 0, 32), (0, 1, 32), (5, 1, 33), (13, 1, 32), (1024, 0, 32),
                             (1536, 0, 32), (2048, 1, 32), (0, 0, 64), (0, 1, 64), (0, 0, 96), (1536, 1, 96),
                             (0, 0, 128), (1, 0, 128), (7, 0, 384), (0, 0, 640), (2048, 0, 896), (0, 0, 129),
                             (0, 0, 192)):

@@ -1612,6 +1612,7 @@ constexpr int kVarWorkgroup = 1 << 16;
 constexpr int kVarRegStaged = 32;
 constexpr int kVarRingP5 = 128 | (3 << 8);
 constexpr int kVarRingP4 = 128;
+constexpr int kVarSorted = 1 << 17; /* group the tile's keys by length (the SORT pipeline) */
 
 int grid_cap()
 {
@@ -1673,17 +1674,10 @@ template <int MODE, bool SORT>
 hipError_t launch_sorted(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                          hipStream_t stream, int var)
 {
-    /* variant bit 0: shift-add FNV multiply (FNV-64 modes); bits 1-2: L2
-     * prefetch distance code; bit 3: no-hash diagnostic (fnv1a_64 unsorted) */
-    if constexpr (has_mul_variant(MODE)) {
-        switch (var & 7) {
-        case 1: return launch_kernel<MODE, SORT, 1>(base, off, delta, nkeys, out, stream);
-        case 3: return launch_kernel<MODE, SORT, 3>(base, off, delta, nkeys, out, stream);
-        case 5: return launch_kernel<MODE, SORT, 5>(base, off, delta, nkeys, out, stream);
-        case 7: return launch_kernel<MODE, SORT, 7>(base, off, delta, nkeys, out, stream);
-        default: break;
-        }
-    }
+    /* variant bit 0: shift-add FNV multiply (FNV-64 modes); bit 3: no-hash
+     * diagnostic (fnv1a_64 unsorted). The L2-prefetch distance (bits 1-2) is
+     * only built into the bit-3 diagnostic: it made the pipeline slower at
+     * every distance. */
     if constexpr (MODE == NC_GPUHASH_FNV1A_64 && !SORT) {
         if (var & 8) {
             switch (var & 6) {
@@ -1693,8 +1687,7 @@ hipError_t launch_sorted(const uint8_t *base, const uint64_t *off, uint64_t delt
             default: return launch_kernel<MODE, SORT, 8>(base, off, delta, nkeys, out, stream);
             }
         }
-        if (var & 16) return (var & 8) ? launch_kernel<MODE, SORT, 24>(base, off, delta, nkeys, out, stream)
-                                       : launch_kernel<MODE, SORT, 16>(base, off, delta, nkeys, out, stream);
+        if (var & 16) return launch_kernel<MODE, SORT, 16>(base, off, delta, nkeys, out, stream);
     }
     if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_MD5) {
         if (var & 64) return (var & 32) ? launch_kernel<MODE, SORT, 32 | 64>(base, off, delta, nkeys, out, stream)
@@ -1706,12 +1699,10 @@ hipError_t launch_sorted(const uint8_t *base, const uint64_t *off, uint64_t delt
         }
         return launch_kernel<MODE, SORT, 32>(base, off, delta, nkeys, out, stream);
     }
-    switch (var & 6) {
-    case 2: return launch_kernel<MODE, SORT, 2>(base, off, delta, nkeys, out, stream);
-    case 4: return launch_kernel<MODE, SORT, 4>(base, off, delta, nkeys, out, stream);
-    case 6: return launch_kernel<MODE, SORT, 6>(base, off, delta, nkeys, out, stream);
-    default: return launch_kernel<MODE, SORT, 0>(base, off, delta, nkeys, out, stream);
+    if constexpr (has_mul_variant(MODE)) {
+        if (var & 1) return launch_kernel<MODE, SORT, 1>(base, off, delta, nkeys, out, stream);
     }
+    return launch_kernel<MODE, SORT, 0>(base, off, delta, nkeys, out, stream);
 }
 
 template <int MODE>
@@ -1765,18 +1756,6 @@ hipError_t launch_wr_x(const uint8_t *base, const uint64_t *off, uint64_t delta,
                        hipStream_t stream, int var)
 {
     const bool w4 = (var & 2048) != 0;
-    if (var & 32768) { /* long keys: 64-key tiles in 8-16 KiB slab slots */
-        switch ((var >> 8) & 7) {
-        case 1: return w4 ? launch_wr_plain<MODE, VAR, 16, 1, 2, 4, 64>(base, off, delta, nkeys, out, stream)
-                          : launch_wr_plain<MODE, VAR, 16, 1, 2, 1, 64>(base, off, delta, nkeys, out, stream);
-        case 2: return w4 ? launch_wr_plain<MODE, VAR, 12, 1, 2, 4, 64>(base, off, delta, nkeys, out, stream)
-                          : launch_wr_plain<MODE, VAR, 12, 1, 2, 1, 64>(base, off, delta, nkeys, out, stream);
-        case 3: return w4 ? launch_wr_plain<MODE, VAR, 8, 2, 3, 4, 64>(base, off, delta, nkeys, out, stream)
-                          : launch_wr_plain<MODE, VAR, 8, 2, 3, 1, 64>(base, off, delta, nkeys, out, stream);
-        default: return w4 ? launch_wr_plain<MODE, VAR, 8, 1, 2, 4, 64>(base, off, delta, nkeys, out, stream)
-                           : launch_wr_plain<MODE, VAR, 8, 1, 2, 1, 64>(base, off, delta, nkeys, out, stream);
-        }
-    }
     if (var & 8192) { /* 64-key tiles, one key per lane */
         switch ((var >> 8) & 7) {
         case 1: return w4 ? launch_wr_plain<MODE, VAR, 2, 1, 2, 4, 64>(base, off, delta, nkeys, out, stream)
@@ -1823,15 +1802,10 @@ template <int MODE>
 hipError_t launch_wr_mode(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                           hipStream_t stream, int var)
 {
-    if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_MD5 || MODE == NC_GPUHASH_CRC32) {
-        if (var & (2048 | 4096 | 8192 | 16384 | 32768)) { /* bit 14: pinned look-ahead reads */
-            const int v = ((var & 4096) ? 512 : 0) | ((var & 16384) ? 1024 : 0);
-            switch (v) {
-            case 512: return launch_wr_x<MODE, 512>(base, off, delta, nkeys, out, stream, var);
-            case 1024: return launch_wr_x<MODE, 1024>(base, off, delta, nkeys, out, stream, var);
-            case 1536: return launch_wr_x<MODE, 1536>(base, off, delta, nkeys, out, stream, var);
-            default: return launch_wr_x<MODE, 0>(base, off, delta, nkeys, out, stream, var);
-            }
+    if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_MD5) {
+        if (var & (2048 | 4096 | 8192)) {
+            if (var & 4096) return launch_wr_x<MODE, 512>(base, off, delta, nkeys, out, stream, var);
+            return launch_wr_x<MODE, 0>(base, off, delta, nkeys, out, stream, var);
         }
         if (var & 8) { /* DIAGNOSTIC no-hash build: default and P5 ring shapes only */
             if (((var >> 8) & 7) == 3) return launch_wr_plain<MODE, 8, 5, 2, 3>(base, off, delta, nkeys, out, stream);
@@ -1932,6 +1906,10 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
         return crc ? kVarWorkgroup : kVarRegStaged;
     }
     if (fixed && mean < 20u) return kVarWorkgroup;
+    /* varying lengths: md5 and the crcs gain from length-grouped waves
+     * (md5: a wave runs a second block if any lane needs one) */
+    if (mode == NC_GPUHASH_MD5) return mean < 28u ? (kVarWorkgroup | kVarSorted) : (kVarRegStaged | kVarSorted);
+    if (crc && mean < 28u) return kVarWorkgroup | kVarSorted;
     return kVarRegStaged;
 }
 
@@ -1941,8 +1919,9 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
     const uintptr_t kp = reinterpret_cast<uintptr_t>(d_keys);
     const uint8_t *base = reinterpret_cast<const uint8_t *>(kp & ~(uintptr_t)15);
     const uint64_t delta = (uint64_t)(kp & 15u);
-    const bool sort = sort_enabled();
-    int var = g_variant != 0 ? g_variant & ~kVarWorkgroup : pick_variant(mode, nkeys, shape) & ~kVarWorkgroup;
+    int var = g_variant != 0 ? g_variant : pick_variant(mode, nkeys, shape);
+    const bool sort = sort_enabled() || (var & kVarSorted) != 0;
+    var &= ~(kVarWorkgroup | kVarSorted);
     /* the wave ring DMAs offsets 16 bytes per lane: it needs 16-byte aligned
      * offsets (any other alignment takes the workgroup pipeline) */
     if ((var & 128) != 0 && (reinterpret_cast<uintptr_t>(d_off) & 15u) != 0) var = g_variant != 0 ? 0 : 32;
