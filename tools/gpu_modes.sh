@@ -1,7 +1,7 @@
 #!/bin/bash
 # All 12 modes on C3 (BASELINE.json configs[2]): in-process variant sweep,
 # rocprofv3 kernel-trace stats, and one FETCH_SIZE / WRITE_SIZE pass each
-# (variant 0). First failure ends the script.   usage: tools/gpu_modes.sh <tag>
+# (variant 0 = the shape policy's pipeline). First failure ends the script.   usage: tools/gpu_modes.sh <tag>
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -14,7 +14,7 @@ step() {
     timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
     local rc=$?; echo "   rc=$rc"; [ $rc -eq 0 ] || tail -n 20 "$OUT/$name.log"; return $rc
 }
-step sweep 500 python3 tools/sweep.py --configs C3 --modes $MODES --variants 0:0:0,0:0:32,0:1:0 --rounds 3 || exit $?
+step sweep 500 python3 tools/sweep.py --configs C3 --modes $MODES --variants 0:0:0,0:0:65536,0:0:32,0:0:896,0:1:65536 --rounds 3 || exit $?
 step trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o modes --output-format csv -- \
     python3 tools/pmc_run.py --config C3 --mode $MODES --variant 0:0:0 --iters 10 || exit $?
 for ctr in FETCH_SIZE WRITE_SIZE; do

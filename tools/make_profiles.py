@@ -70,10 +70,11 @@ def modes(src, rnd):
         m["sweep_ms_median"][key] = r["ms_median"]
     stats = os.path.join(src, "trace", "modes_kernel_stats.csv")
     for r in csv.DictReader(open(stats)):
-        mm = re.search(r"nc_hash_kernel<(\d+), (true|false), (\d+)>", r["Name"])
+        mm = re.search(r"(nc_hash_kernel(?:_rs|_wr)?)<(\d+), ([^>]*)>", r["Name"])
         if mm:
-            name = MODE_NAMES[int(mm.group(1))]
-            res["modes"][name]["trace_avg_ms_var0"] = round(float(r["AverageNs"]) / 1e6, 4)
+            name = MODE_NAMES[int(mm.group(2))]
+            res["modes"][name]["trace_kernel"] = f"{mm.group(1)}<{mm.group(2)}, {mm.group(3)}>"
+            res["modes"][name]["trace_avg_ms_auto"] = round(float(r["AverageNs"]) / 1e6, 4)
             res["modes"][name]["trace_calls"] = int(r["Calls"])
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         for k, v in counters(os.path.join(src, f"pmc_{ctr}", "pmc_counter_collection.csv")).items():
@@ -81,10 +82,10 @@ def modes(src, rnd):
             if mm:
                 res["modes"][MODE_NAMES[int(mm.group(1))]][ctr + "_KB"] = v[ctr]
     for name, m in res["modes"].items():
-        v0 = m["sweep_ms_median"].get("grid0_sort0_var0")
+        v0 = m["sweep_ms_median"].get("grid0_sort0_var0")  # var 0 = the shape policy's choice
         if v0:
-            m["alg_gbs_var0"] = round(alg / (v0 * 1e-3) / 1e9, 1)
-            m["frac_var0"] = round(m["alg_gbs_var0"] / 8000.0, 4)
+            m["alg_gbs_auto"] = round(alg / (v0 * 1e-3) / 1e9, 1)
+            m["frac_auto"] = round(m["alg_gbs_auto"] / 8000.0, 4)
         if "FETCH_SIZE_KB" in m and "WRITE_SIZE_KB" in m:
             m["hbm_bytes_per_launch"] = round(2.0 * m["FETCH_SIZE_KB"] * 1024 + m["WRITE_SIZE_KB"] * 1024)
             m["traffic_over_alg"] = round(m["hbm_bytes_per_launch"] / alg, 4)

@@ -23,9 +23,9 @@ def short(name: str) -> str:
     m = re.search(r"(nc_hash_kernel(?:_rs)?)<(\d+), (true|false), (\d+)>", name)
     if m:
         return f"{m.group(1)}<mode={m.group(2)},sort={m.group(3)},var={m.group(4)}>"
-    m = re.search(r"(nc_hash_kernel_wr)<([-\d, ]+)>", name)
+    m = re.search(r"(nc_hash_kernel_wr)<(\d+), ([-\d, ]+)>", name)
     if m:
-        return f"{m.group(1)}<{m.group(2)}>"
+        return f"{m.group(1)}<mode={m.group(2)},{m.group(3).replace(' ', '')}>"
     return name.replace("void (anonymous namespace)::", "").split("(")[0][:80]
 
 

@@ -1664,6 +1664,7 @@ hipError_t launch_kernel(const uint8_t *base, const uint64_t *off, uint64_t delt
     const int cap = grid_cap();
     uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu;
     if (grid > ntiles) grid = ntiles;
+    (void)hipGetLastError(); /* a stale error from another library's call must not be reported as ours */
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, stream, base, off, delta, nkeys, out, ntiles);
     return hipGetLastError();
 }
@@ -1735,6 +1736,7 @@ hipError_t launch_wr(const uint8_t *base, const uint64_t *off, uint64_t delta, u
     const int cap = grid_cap();
     uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu;
     if (grid > max_grid) grid = max_grid;
+    (void)hipGetLastError(); /* a stale error from another library's call must not be reported as ours */
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * WPW), lds, stream, base, off, delta, nkeys, out, ntiles,
                        dist);
     return hipGetLastError();
@@ -1856,6 +1858,7 @@ hipError_t dist_launch(const uint8_t *base, const uint64_t *off, uint64_t delta,
     uint64_t grid = (nkeys + 255u) / 256u;
     const uint64_t cap = (uint64_t)num_cus() * 8u;
     if (grid > cap) grid = cap;
+    (void)hipGetLastError();
     if (d.kind == 0)
         hipLaunchKernelGGL(nc_dispatch_kernel<kDistKetama>, dim3((unsigned)grid), dim3(256), 0, stream, d.cont, d.ncont,
                            out, nkeys);
