@@ -240,3 +240,43 @@ def test_sort_and_grid_variants_agree_full_size(gpu):
         ref = ref or h
         assert h == ref, (grid, sort, var)
     L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
+def test_key_buffers_beyond_4gib(gpu):
+    """4.25 GiB of 256-B keys (offsets past 2^31 and 2^32; C4's shard is 8 GiB):
+    every pipeline and the fused server_idx, sampled keys around both marks
+    against the per-key host symbols. (A signed readfirstlane once sign-
+    extended the ring's tile bounds past 2 GiB.)"""
+    import torch
+
+    spec = t.SynthSpec.fixed(4, 256)
+    n = (1 << 24) + (1 << 20)
+    kd, od = t.synth_device(spec, 0, n)
+    rng = np.random.default_rng(5)
+    sample = sorted({0, n - 1} | {(1 << 23) + d for d in (-1, 0, 1)} | {(1 << 24) + d for d in (-1, 0, 1)} |
+                    {int(x) for x in rng.integers(0, n, size=24)})
+    host = {i: t.synth_host(spec, i, 1)[0][:256].tobytes() for i in sample}
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    try:
+        for var in (0, 65536, 32, 128, 896, 2176):
+            L.lib().nc_gpuhash_set_tuning(0, 0, var)
+            for name in ("md5", "crc32", "fnv1a_64"):
+                t.hash_batch_device(name, kd, od, out, shape=spec.shape(256 * n))
+                torch.cuda.synchronize()
+                h = out.cpu().numpy().view(np.uint32)
+                for i in sample:
+                    assert int(h[i]) == t.hash_key(name, host[i]), (var, name, i)
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+    cont = t.continuum_device(np.arange(8, dtype=np.uint32) % 4, np.arange(8, dtype=np.uint32) << 29)
+    for shape in (None, spec.shape(256 * n)):
+        got = t.server_idx_device("fnv1a_64", "ketama", kd, od, cont, 4, shape=shape)
+        torch.cuda.synchronize()
+        g = got.cpu().numpy().view(np.uint32)
+        vals = np.arange(8, dtype=np.uint32) << 29
+        for i in sample:
+            hv = t.hash_key("fnv1a_64", host[i])
+            p = int(np.searchsorted(vals, hv, side="left")) % 8
+            assert int(g[i]) == p % 4, (shape, i)
+    del kd, od, out
+    torch.cuda.empty_cache()

@@ -79,3 +79,19 @@ def test_lds_fits_eight_workgroups(asm_file):
             continue
         lds = int([l for l in block.splitlines() if ".amdhsa_group_segment_fixed_size" in l][0].split()[-1])
         assert lds * 8 <= 160 * 1024, (name, lds)
+
+
+def test_ring_bounds_are_not_sign_extended(asm_file):
+    """The wave ring builds 64-bit tile bounds from readfirstlane'd dwords;
+    readfirstlane returns int, and an s_ashr_i32 there sign-extends a low
+    dword >= 2^31 over the high one (a fault past 2 GiB of keys)."""
+    import re
+
+    cur, bad = None, []
+    for line in open(asm_file):
+        m = re.match(r"^(_Z\S+):", line)
+        if m:
+            cur = m.group(1)
+        elif cur and "nc_hash_kernel_wr" in cur and line.strip().startswith("s_ashr_i32"):
+            bad.append(cur)
+    assert not bad, sorted(set(bad))[:3]

@@ -1261,9 +1261,14 @@ __device__ __forceinline__ uint32_t wr_count(uint64_t tile, uint64_t nkeys)
 template <int TK>
 __device__ __forceinline__ void wr_bounds(const uint32_t *ob, uint64_t delta, uint64_t &S, uint64_t &E)
 {
-    S = (((uint64_t)__builtin_amdgcn_readfirstlane(ob[1]) << 32) | __builtin_amdgcn_readfirstlane(ob[0])) + delta;
-    E = (((uint64_t)__builtin_amdgcn_readfirstlane(ob[2 * TK + 1]) << 32) |
-         __builtin_amdgcn_readfirstlane(ob[2 * TK])) + delta;
+    /* readfirstlane returns int: through uint32_t, or a low dword >= 2^31
+     * sign-extends over the high one (key buffers past 2 GiB) */
+    const uint32_t s_lo = (uint32_t)__builtin_amdgcn_readfirstlane(ob[0]);
+    const uint32_t s_hi = (uint32_t)__builtin_amdgcn_readfirstlane(ob[1]);
+    const uint32_t e_lo = (uint32_t)__builtin_amdgcn_readfirstlane(ob[2 * TK]);
+    const uint32_t e_hi = (uint32_t)__builtin_amdgcn_readfirstlane(ob[2 * TK + 1]);
+    S = (((uint64_t)s_hi << 32) | s_lo) + delta;
+    E = (((uint64_t)e_hi << 32) | e_lo) + delta;
 }
 
 /* hash_tag trimming of server_pool_idx (src/nc_server.c:665-677): the first
@@ -1387,7 +1392,7 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
 
     const uint32_t t = threadIdx.x;
     const uint32_t lane = t & 63u;
-    const uint32_t wave = WPW == 1 ? 0u : __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint32_t wave = WPW == 1 ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane(t >> 6);
     uint8_t *smem = wr_lds + wave * R::kBytes;
     uint32_t *tab = reinterpret_cast<uint32_t *>(wr_lds + kTabOffs);
     uint32_t *cont = reinterpret_cast<uint32_t *>(wr_lds + kContOffs);
