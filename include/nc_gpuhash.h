@@ -150,6 +150,44 @@ rstatus_t nc_gpuhash_ketama_build_device(const char *const *names, const uint32_
                                          struct nc_gpuhash_continuum *d_continuum, uint32_t cap,
                                          uint32_t *ncontinuum, void *stream);
 
+/* ---- 3a''. key extraction on the device ----
+ * A stream of pipelined memcache retrieval requests ("get k1 k2 ...\r\n",
+ * "gets ...\r\n": memcache_parse_req, src/proto/nc_memcache.c:219-447,
+ * :709-717) into the key CSR the batch entry points take. Every complete
+ * request line is parsed in parallel; keys are produced for the requests
+ * before the first one that is malformed (the reference would close the
+ * connection there) or is not a retrieval command (its data block is not a
+ * line: the host parser takes over from `consumed`). */
+typedef struct nc_gpuhash_mc_parser nc_gpuhash_mc_parser_t;
+
+#define NC_GPUHASH_MC_OK            0
+#define NC_GPUHASH_MC_EINVAL       -1 /* syntax the reference rejects */
+#define NC_GPUHASH_MC_EKEYLEN      -2 /* empty key or longer than 250 bytes (nc_memcache.c:33) */
+#define NC_GPUHASH_MC_EUNSUPPORTED -3 /* a request type other than get / gets */
+
+struct nc_gpuhash_mc_result {
+    uint64_t nreqs;       /* complete ("...\r\n") request lines in the stream */
+    uint64_t nkeys;       /* keys written (requests [0, first_error)) */
+    uint64_t first_error; /* index of the first request not parsed here, or nreqs */
+    uint64_t consumed;    /* stream bytes of requests [0, first_error) */
+};
+
+/* Device workspace for streams up to max_bytes (< 2^31), max_reqs complete
+ * requests and max_keys keys. NULL with errno on failure. */
+nc_gpuhash_mc_parser_t *nc_gpuhash_mc_parser_create(uint64_t max_bytes, uint64_t max_reqs, uint64_t max_keys);
+void nc_gpuhash_mc_parser_destroy(nc_gpuhash_mc_parser_t *ps);
+
+/* Parse d_stream[0, nbytes). Writes the packed keys (d_keys, NULL = spans
+ * only; needs result->nkeys's bytes + NC_GPUHASH_PAD), d_offsets (nkeys + 1),
+ * the request index of each key (d_key_req, may be NULL) and each request's
+ * NC_GPUHASH_MC_* status (d_req_status, nreqs entries, may be NULL). Blocks
+ * until done (the counts size the next launch). NC_ENOMEM when a limit of the
+ * workspace is exceeded. */
+rstatus_t nc_gpuhash_mc_parse_device(nc_gpuhash_mc_parser_t *ps, const uint8_t *d_stream, uint64_t nbytes,
+                                     uint8_t *d_keys, uint64_t *d_offsets, uint32_t *d_key_req,
+                                     int32_t *d_req_status, struct nc_gpuhash_mc_result *result,
+                                     void *stream);
+
 /* The launch variant the auto policy picks for this mode and shape (the
  * variant bits of nc_gpuhash_set_tuning; bit 16 = the plain workgroup
  * pipeline); -1 with errno EINVAL for an invalid mode. */

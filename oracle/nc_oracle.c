@@ -576,3 +576,72 @@ int oracle_server_idx_batch(int mode, int dist, const uint32_t *values, const ui
     }
     return 0;
 }
+
+/*
+ * memcache_parse_req (src/proto/nc_memcache.c) for a stream of retrieval
+ * requests, sequentially, as the reference walks it: SW_START (:219-232),
+ * SW_REQ_TYPE (:234-368; get :245, gets :268, CR after them :343-345),
+ * SW_SPACES_BEFORE_KEY (:372-378), SW_KEY (:380-428; empty or > 250 bytes
+ * :384-396; a CR is re-read :421-426), SW_SPACES_BEFORE_KEYS (:431-447),
+ * SW_ALMOST_DONE (:709-717). Stops at the first request that is malformed
+ * (-1: syntax, -2: key length) or not get/gets (-3), or at an incomplete
+ * last request. Writes key spans of the accepted requests and each parsed
+ * request's status; returns 0.
+ */
+int oracle_mc_parse(const uint8_t *s, uint64_t n, uint64_t max_keys, uint64_t *kstart, uint32_t *klen,
+                    uint32_t *kreq, int32_t *status, uint64_t max_reqs, uint64_t *nkeys, uint64_t *nreqs_parsed,
+                    uint64_t *first_error, uint64_t *consumed)
+{
+    uint64_t p = 0, nk = 0, nr = 0, done = 0;
+    *first_error = UINT64_MAX;
+    for (;;) {
+        /* a request is complete only with its CR LF; find it (keys hold no CR) */
+        uint64_t e = p;
+        while (e + 1 < n && !(s[e] == '\r' && s[e + 1] == '\n')) e++;
+        if (e + 1 >= n) break; /* incomplete: left for the next read */
+        if (nr >= max_reqs) return -1;
+        int32_t st = 0;
+        uint64_t q = p, kn = 0;
+        while (q < e && s[q] == ' ') q++;                            /* SW_START */
+        const uint64_t t0 = q;
+        while (q < e && s[q] >= 'a' && s[q] <= 'z') q++;            /* SW_REQ_TYPE */
+        const uint64_t tl = q - t0;
+        if (tl == 0 || (q < e && s[q] != ' ')) {
+            st = -1;
+        } else if (!((tl == 3 && memcmp(s + t0, "get", 3) == 0) || (tl == 4 && memcmp(s + t0, "gets", 4) == 0))) {
+            st = -3;
+        } else if (q == e) {
+            st = -1; /* "get\r\n" */
+        } else {
+            while (q < e && s[q] == ' ') q++;                        /* SW_SPACES_BEFORE_KEY */
+            for (;;) {
+                if (q < e && s[q] == '\r') { st = -1; break; }      /* SW_ALMOST_DONE wants LF */
+                const uint64_t k0 = q;                               /* SW_KEY */
+                while (q < e && s[q] != ' ' && s[q] != '\r') q++;
+                if (q - k0 == 0 || q - k0 > 250) { st = -2; break; }
+                if (nk + kn >= max_keys) return -1;
+                kstart[nk + kn] = k0;
+                klen[nk + kn] = (uint32_t)(q - k0);
+                kreq[nk + kn] = (uint32_t)nr;
+                kn++;
+                if (q < e && s[q] == '\r') { st = -1; break; }
+                while (q < e && s[q] == ' ') q++;                    /* SW_SPACES_BEFORE_KEYS */
+                if (q == e) break;
+            }
+        }
+        status[nr] = st;
+        nr++;
+        if (st != 0) {
+            *first_error = nr - 1;
+            break;
+        }
+        nk += kn;
+        p = e + 2;
+        done = p;
+    }
+    *nkeys = nk;
+    *nreqs_parsed = nr;
+    if (*first_error == UINT64_MAX) *first_error = nr;
+    *consumed = done;
+    return 0;
+}

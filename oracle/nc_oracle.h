@@ -89,6 +89,12 @@ int oracle_server_idx_batch(int mode, int dist, const uint32_t *values, const ui
                             uint32_t ncont, uint32_t nserver, const char *tag,
                             const uint8_t *keys, const uint64_t *offsets, uint64_t nkeys, uint32_t *out);
 
+/* memcache_parse_req (src/proto/nc_memcache.c) over a stream of retrieval
+ * requests, sequentially; see nc_oracle.c. Returns 0, or -1 when a limit is hit. */
+int oracle_mc_parse(const uint8_t *s, uint64_t n, uint64_t max_keys, uint64_t *kstart, uint32_t *klen,
+                    uint32_t *kreq, int32_t *status, uint64_t max_reqs, uint64_t *nkeys, uint64_t *nreqs_parsed,
+                    uint64_t *first_error, uint64_t *consumed);
+
 #ifdef __cplusplus
 }
 #endif

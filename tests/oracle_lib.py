@@ -40,6 +40,10 @@ class Oracle:
         lib.oracle_ketama_build.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint32),
                                             ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_uint32]
+        lib.oracle_mc_parse.restype = ctypes.c_int
+        lib.oracle_mc_parse.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         lib.oracle_ketama_build_live.restype = ctypes.c_int
         lib.oracle_ketama_build_live.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint32),
                                                  ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p, ctypes.c_uint32,
@@ -103,6 +107,22 @@ class Oracle:
                                            idx.ctypes.data, cap)
         assert cnt >= 0
         return idx[:cnt]
+
+    def mc_parse(self, stream: bytes, max_keys: int = 1 << 20, max_reqs: int = 1 << 20):
+        """memcache retrieval-request stream -> (key spans [(start, len)], key_req, statuses, info)."""
+        buf = np.frombuffer(stream, dtype=np.uint8) if len(stream) else np.zeros(1, np.uint8)
+        ks = np.zeros(max_keys, np.uint64)
+        kl = np.zeros(max_keys, np.uint32)
+        kr = np.zeros(max_keys, np.uint32)
+        st = np.zeros(max_reqs, np.int32)
+        out = (ctypes.c_uint64 * 4)()
+        rc = self.lib.oracle_mc_parse(buf.ctypes.data, len(stream), max_keys, ks.ctypes.data, kl.ctypes.data,
+                                      kr.ctypes.data, st.ctypes.data, max_reqs, ctypes.byref(out, 0),
+                                      ctypes.byref(out, 8), ctypes.byref(out, 16), ctypes.byref(out, 24))
+        assert rc == 0
+        nk, nr = int(out[0]), int(out[1])
+        info = {"nkeys": nk, "nparsed": nr, "first_error": int(out[2]), "consumed": int(out[3])}
+        return ks[:nk], kl[:nk], kr[:nk], st[:nr], info
 
     def modula_dispatch(self, idx: np.ndarray, h: int) -> int:
         return int(self.lib.oracle_modula_dispatch(idx.ctypes.data, idx.size, h))

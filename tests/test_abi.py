@@ -186,3 +186,12 @@ def test_ketama_build_argument_errors():
     assert cnt.value == 0
     # more points than cap: NC_ENOMEM before any device work
     assert f(names, lens, (ctypes.c_uint32 * 2)(1, 1), None, 2, None, 10, ctypes.byref(cnt), None) == L.NC_ENOMEM
+
+
+def test_mc_parser_argument_errors():
+    lib = L.lib()
+    for args in ((0, 1, 1), (1, 0, 1), (1, 1, 0), (1 << 31, 1, 1)):
+        ctypes.set_errno(0)
+        assert not lib.nc_gpuhash_mc_parser_create(*args)
+        assert ctypes.get_errno() == errno.EINVAL
+    assert lib.nc_gpuhash_mc_parse_device(None, None, 0, None, None, None, None, None, None) == L.NC_ERROR

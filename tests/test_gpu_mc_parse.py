@@ -1,0 +1,107 @@
+"""Key extraction on the device: nc_gpuhash_mc_parse_device
+against the oracle's sequential restatement of memcache_parse_req for
+retrieval requests (src/proto/nc_memcache.c:219-447, :709-717), then the
+extracted CSR through the hash kernels."""
+import numpy as np
+import pytest
+
+import twemproxy_amd as t
+
+pytestmark = pytest.mark.gpu
+
+ALPHA = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789:_-.{}ABC\n\x01\xff", dtype=np.uint8)
+
+
+def dev(b: bytes):
+    import torch
+
+    return torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy()).cuda() if b else \
+        torch.zeros(0, dtype=torch.uint8, device="cuda")
+
+
+def check(parser, oracle, stream: bytes):
+    import torch
+
+    keys, off, kreq, status, info = parser.parse(dev(stream))
+    torch.cuda.synchronize()
+    ks, kl, kr, st, oi = oracle.mc_parse(stream)
+    assert info["nreqs"] == stream.count(b"\r\n") or b"\r\r\n" in stream
+    assert info["first_error"] == oi["first_error"], (info, oi)
+    assert info["consumed"] == oi["consumed"]
+    assert info["nkeys"] == oi["nkeys"]
+    o = off.cpu().numpy()
+    kb = keys.cpu().numpy()
+    want = [stream[int(a): int(a) + int(n)] for a, n in zip(ks, kl)]
+    got = [kb[o[i]: o[i + 1]].tobytes() for i in range(len(o) - 1)]
+    assert got == want
+    np.testing.assert_array_equal(kreq.cpu().numpy().astype(np.uint32), kr)
+    fe = oi["first_error"]
+    np.testing.assert_array_equal(status.cpu().numpy()[: len(st)], st)
+    return keys, off, info
+
+
+@pytest.fixture(scope="module")
+def parser():
+    p = t.McParser(max_bytes=1 << 24, max_reqs=1 << 20, max_keys=1 << 20)
+    yield p
+    p.close()
+
+
+@pytest.mark.parametrize("stream,nkeys,first_error", [
+    (b"", 0, 0),
+    (b"get a\r\n", 1, 1),
+    (b"get a bb ccc\r\n", 3, 1),
+    (b"gets a\r\n  get   b  \r\n", 2, 2),           # spaces before type, around keys
+    (b"get a\r\nget b", 1, 1),                     # incomplete last request: left for the next read
+    (b"get \r\n", 0, 0),                            # empty key (nc_memcache.c:391-395)
+    (b"get\r\n", 0, 0),                             # CR right after get (:343-345)
+    (b"GET a\r\n", 0, 0),                           # type must be lowercase (:224-226)
+    (b"get\ta\r\n", 0, 0),                          # not a space after the type
+    (b"get a\rb\r\n", 0, 0),                        # CR without LF (:709-717)
+    (b"get a\nb\r\n", 1, 1),                        # LF inside a key is a key byte
+    (b"get " + b"k" * 250 + b"\r\n", 1, 1),         # MEMCACHE_MAX_KEY_LENGTH (:33)
+    (b"get " + b"k" * 251 + b"\r\n", 0, 0),
+    (b"get a\r\nset k 0 0 1\r\nx\r\nget b\r\n", 1, 1),  # storage command: host parser takes over
+    (b"get a\r\ndelete b\r\n", 1, 1),
+    (b"\r\nget a\r\n", 0, 0),
+])
+def test_reference_vectors(gpu, oracle, parser, stream, nkeys, first_error):
+    _, _, info = check(parser, oracle, stream)
+    assert info["nkeys"] == nkeys and info["first_error"] == first_error
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_pipelines(gpu, oracle, parser, seed):
+    """C5-shaped pipelines (1-12 keys per request, Zipf-ish lengths, runs of
+    spaces), with a malformed request injected for odd seeds."""
+    rng = np.random.default_rng(seed)
+    reqs = []
+    for r in range(3000):
+        nk = int(rng.integers(1, 13))
+        words = [rng.choice(ALPHA[:-5] if seed % 3 else ALPHA, size=int(min(250, 1 + rng.zipf(1.3)))).tobytes()
+                 for _ in range(nk)]
+        words = [w.replace(b"\r", b"") for w in words]
+        sp = [b" " * int(rng.integers(1, 3)) for _ in range(nk)]
+        cmd = b"gets" if rng.random() < 0.2 else b"get"
+        reqs.append(b" " * int(rng.integers(0, 2)) + cmd + b"".join(s + w for s, w in zip(sp, words)) + b"\r\n")
+    if seed % 2:
+        i = int(rng.integers(100, 2900))
+        reqs[i] = [b"get \r\n", b"get " + b"x" * 300 + b"\r\n", b"set a 0 0 1\r\n", b"get a\rb\r\n"][seed % 4]
+    stream = b"".join(reqs) + b"get partial"
+    check(parser, oracle, stream)
+
+
+def test_extracted_keys_hash_like_the_host(gpu, oracle, parser):
+    """parse -> fnv1a_64 / md5 on the extracted CSR == per-key host hash_t."""
+    import torch
+
+    spec = t.SynthSpec.zipf(5, charset=t.BYTES_PRINTABLE)
+    kh, oh = t.synth_host(spec, 0, 8192)
+    keys = [kh[oh[i]: oh[i + 1]].tobytes() for i in range(8192)]
+    stream = b"".join(b"get " + k + b"\r\n" for k in keys)  # 64 conns x 128 pipelined gets (C5)
+    kd, od, info = check(parser, oracle, stream)
+    assert info["nkeys"] == 8192
+    for name in ("fnv1a_64", "md5", "crc32"):
+        h = t.hash_batch_device(name, kd, od)
+        torch.cuda.synchronize()
+        assert h.cpu().numpy().view(np.uint32).tolist() == [t.hash_key(name, k) for k in keys], name

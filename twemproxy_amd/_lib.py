@@ -42,6 +42,13 @@ class NcShape(ctypes.Structure):
     _fields_ = [("key_bytes", ctypes.c_uint64), ("min_len", ctypes.c_uint32), ("max_len", ctypes.c_uint32)]
 
 
+class NcMcResult(ctypes.Structure):
+    """struct nc_gpuhash_mc_result (include/nc_gpuhash.h)."""
+
+    _fields_ = [("nreqs", ctypes.c_uint64), ("nkeys", ctypes.c_uint64), ("first_error", ctypes.c_uint64),
+                ("consumed", ctypes.c_uint64)]
+
+
 class NcKeySpan(ctypes.Structure):
     """struct nc_keyspan — the shape of twemproxy's struct keypos (src/nc_message.h:232-235)."""
 
@@ -89,6 +96,13 @@ SIGNATURES = {
         [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
          ctypes.c_void_p],
+    ),
+    "nc_gpuhash_mc_parser_create": (ctypes.c_void_p, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
+    "nc_gpuhash_mc_parser_destroy": (None, [ctypes.c_void_p]),
+    "nc_gpuhash_mc_parse_device": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.POINTER(NcMcResult), ctypes.c_void_p],
     ),
     "nc_gpuhash_pick_variant": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(NcShape)]),
     "nc_gpuhash_time_device_shaped": (

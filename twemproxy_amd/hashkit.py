@@ -222,6 +222,56 @@ def server_idx_device(hash_: int | str, dist: int | str, keys, offsets, continuu
     return out
 
 
+MC_OK, MC_EINVAL, MC_EKEYLEN, MC_EUNSUPPORTED = 0, -1, -2, -3  # NC_GPUHASH_MC_*
+
+
+class McParser:
+    """Key extraction on the device from pipelined memcache retrieval requests
+    (nc_gpuhash_mc_parse_device; memcache_parse_req, src/proto/nc_memcache.c)."""
+
+    def __init__(self, max_bytes: int, max_reqs: int, max_keys: int):
+        self._lib = L.lib()
+        self._h = self._lib.nc_gpuhash_mc_parser_create(max_bytes, max_reqs, max_keys)
+        if not self._h:
+            raise L.NcError(ctypes.get_errno(), "nc_gpuhash_mc_parser_create failed")
+        self.max_keys, self.max_reqs, self.max_bytes = max_keys, max_reqs, max_bytes
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.nc_gpuhash_mc_parser_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def parse(self, stream, stream_handle=None):
+        """stream: uint8 CUDA tensor of requests. Returns (keys uint8 padded,
+        offsets int64 (nkeys+1), key_req int32, req_status int32, result dict);
+        keys/offsets feed hash_batch_device / server_idx_device directly."""
+        import torch
+
+        dev = stream.device
+        nbytes = stream.numel()
+        keys = torch.empty(nbytes + L.NC_GPUHASH_PAD, dtype=torch.uint8, device=dev)
+        off = torch.empty(self.max_keys + 1, dtype=torch.int64, device=dev)
+        kreq = torch.empty(self.max_keys, dtype=torch.int32, device=dev)
+        status = torch.empty(self.max_reqs, dtype=torch.int32, device=dev)
+        res = L.NcMcResult()
+        L.check(
+            self._lib.nc_gpuhash_mc_parse_device(
+                self._h, stream.data_ptr(), nbytes, keys.data_ptr(), off.data_ptr(), kreq.data_ptr(),
+                status.data_ptr(), ctypes.byref(res), _stream_handle(stream_handle),
+            ),
+            "nc_gpuhash_mc_parse_device",
+        )
+        nk, nr = int(res.nkeys), int(res.nreqs)
+        info = {"nreqs": nr, "nkeys": nk, "first_error": int(res.first_error), "consumed": int(res.consumed)}
+        return keys, off[: nk + 1], kreq[:nk], status[:nr], info
+
+
 def time_batch_device(hash_: int | str, keys, offsets, out, iters: int, stream=None, shape=None) -> float:
     """Mean ms per launch over `iters` launches, timed by hipEvents on the launch stream."""
     mode = mode_of(hash_)
