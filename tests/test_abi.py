@@ -141,7 +141,8 @@ def test_auto_policy_choices():
     assert t.pick_variant("fnv1a_64", n, (19 * n, 8, 64)) == RS  # C2 (Zipf)
     assert t.pick_variant("fnv1a_64", n, (36 * n, 8, 64)) == RS  # uniform 8-64
     SORTED = 1 << 17
-    assert t.pick_variant("md5", n, (19 * n, 8, 64)) == WG | SORTED
+    assert t.pick_variant("md5", n, (19 * n, 8, 64)) == 128 | 16384  # C2: in-wave length sort
+    assert t.pick_variant("md5", n, (24 * n, 8, 64)) == WG | SORTED
     assert t.pick_variant("md5", n, (36 * n, 8, 64)) == RS | SORTED
     assert t.pick_variant("crc32", n, (19 * n, 8, 64)) == WG | SORTED
     assert t.pick_variant("crc32a", n, (36 * n, 8, 64)) == RS

@@ -1199,20 +1199,28 @@ struct WrDist {
     uint32_t tag;         /* hash_tag c0 | c1 << 8 | 1 << 16, or 0 for none */
 };
 
+/* TK = 256 (four keys per lane) sorts the tile's keys by length inside the
+ * wave and hashes them in four rounds of 64 similar lengths: a round runs as
+ * long as its longest key, so Zipf lengths cost ~the sum of the four quartile
+ * maxima instead of four times the tile maximum. */
 template <int P, int DS, int DO, int TK = kWrTile>
 struct WrRing {
     static_assert(DO > DS && DS >= 1 && DO >= 2 * DS - 1, "offsets must run far enough ahead of slabs");
-    static_assert(TK == 64 || TK == 128, "a wave tile is one or two keys per lane");
+    static_assert(TK == 64 || TK == 128 || TK == 256, "a wave tile is one, two or four keys per lane");
     static constexpr uint32_t kOffSlot = 8u * TK + 16u;  /* off[k0 .. k0+TK) + end bound, 16-aligned */
     static constexpr int NST = TK / 64;                  /* output stores per tile */
+    static constexpr int NOFF = TK == 256 ? 2 : 1;       /* 16-B offset DMAs per lane per tile */
+    static constexpr int kIter = P + NOFF + 1 + NST;     /* VMEM instructions per iteration, fixed */
     static constexpr uint32_t NS = DS + 1;            /* slab slots: tiles j .. j+DS */
     static constexpr uint32_t NO = DO + 1;            /* offset slots: tiles j .. j+DO */
     static constexpr uint32_t kSlot = (uint32_t)P * 1024u;
     static constexpr uint32_t kOffOffs = NS * kSlot;  /* slab over-reads land in the next slot / the offsets */
     static constexpr uint32_t kOffDump = kOffOffs + NO * kOffSlot;
-    static constexpr uint32_t kBytes = kOffDump + 16u;
-    static constexpr int kWaitOff = (DO - DS) * (P + 2 + NST);
-    static constexpr int kWaitSlab = DS * (P + 2 + NST);
+    static constexpr uint32_t kSortOffs = kOffDump + 16u; /* TK 256: u32 hist[64] + u32 order[256] */
+    static constexpr uint32_t kBytes = kSortOffs + (TK == 256 ? 4u * (64u + 256u) : 0u);
+    static constexpr int kWaitOff = (DO - DS) * kIter;
+    static constexpr int kWaitSlab = DS * kIter;
+    static_assert(kWaitSlab <= 63 && kWaitOff <= 63, "vmcnt is 6 bits");
 };
 
 typedef __attribute__((address_space(3))) const void lds_cvoid_t;
@@ -1429,16 +1437,19 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
     /* OFF(tile) into offset slot `oslot`: 2 instructions */
     auto issue_off = [&](uint64_t tile, uint32_t oslot) __attribute__((always_inline)) {
         if (tile >= ntiles) {
-            dummy(off + nkeys);
-            dummy(off + nkeys);
+#pragma unroll
+            for (int h = 0; h <= R::NOFF; h++) dummy(off + nkeys);
             return;
         }
         const uint64_t k0 = tile * (uint64_t)TK;
         const uint64_t last_pair = (nkeys - 1u) & ~(uint64_t)1; /* pairs (p, p+1) stay <= nkeys */
-        uint64_t p = k0 + 2u * lane;
-        if (p > last_pair) p = last_pair;
         const uint32_t dst = smem_lds + R::kOffOffs + oslot * kWrOffSlot;
-        if (TK == 128 || lane < (uint32_t)TK / 2u) glds16<kNT>(off + p, dst);
+#pragma unroll
+        for (int h = 0; h < R::NOFF; h++) {
+            uint64_t p = k0 + 128u * (uint32_t)h + 2u * lane;
+            if (p > last_pair) p = last_pair;
+            if (TK >= 128 || lane < (uint32_t)TK / 2u) glds16<kNT>(off + p, dst + 1024u * (uint32_t)h);
+        }
         if (lane < 2u) {
             const uint64_t e = k0 + wr_count<TK>(tile, nkeys);
             glds4(reinterpret_cast<const uint32_t *>(off + e) + lane, dst + 8u * TK);
@@ -1505,6 +1516,9 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
         const uint64_t k0 = tile * (uint64_t)TK;
 
         uint32_t h[R::NST];
+        uint32_t key_of[R::NST]; /* tile index of the key each round hashes */
+#pragma unroll
+        for (int q = 0; q < R::NST; q++) key_of[q] = lane + 64u * (uint32_t)q;
         constexpr bool kPair = TK == 128 && (VAR & 512) != 0 && DIST == kDistNone && MODE != NC_GPUHASH_HSIEH &&
                                MODE != NC_GPUHASH_MURMUR && MODE != NC_GPUHASH_JENKINS;
         if constexpr (kPair) {
@@ -1526,9 +1540,41 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
                 goto stores;
             }
         }
+        if constexpr (TK == 256) {
+            /* counting sort of the tile's 256 keys by length class, in LDS:
+             * one wave, so its LDS operations retire in order */
+            uint32_t *hist = reinterpret_cast<uint32_t *>(smem + R::kSortOffs);
+            uint32_t *order = hist + 64;
+            uint32_t bk[4], rk[4];
+            hist[lane] = 0u;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t i = key_of[q];
+                const uint32_t ie = i + 1u >= cnt ? (uint32_t)TK : i + 1u;
+                const uint32_t len = i < cnt ? ob[2u * ie] - ob[2u * i] : 0u;
+                bk[q] = i < cnt ? (len < 62u ? len : 62u) : 63u; /* absent keys last */
+                rk[q] = __hip_atomic_fetch_add(hist + bk[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const uint32_t c = hist[lane];
+            uint32_t incl = c;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t v = __shfl_up(incl, d, 64);
+                if (lane >= (uint32_t)d) incl += v;
+            }
+            hist[lane] = incl - c; /* first rank of length class `lane` */
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < 4; q++) order[hist[bk[q]] + rk[q]] = key_of[q];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < 4; q++) key_of[q] = order[64u * (uint32_t)q + lane];
+        }
 #pragma unroll
         for (int q = 0; q < R::NST; q++) {
-            const uint32_t i = lane + 64u * (uint32_t)q;
+            const uint32_t i = key_of[q];
             const bool valid = i < cnt;
             const uint32_t ie = i + 1u >= cnt ? (uint32_t)TK : i + 1u; /* key cnt-1 ends at the end bound */
             const uint32_t s = ob[2u * i];
@@ -1550,7 +1596,7 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
     stores:
 #pragma unroll
         for (int q = 0; q < R::NST; q++) {
-            const uint32_t i = lane + 64u * (uint32_t)q;
+            const uint32_t i = key_of[q];
             asm_st32<kNT>(i < cnt ? (void *)(out + k0 + i) : (void *)sink, h[q]);
         }
     }
@@ -1618,6 +1664,7 @@ constexpr int kVarRegStaged = 32;
 constexpr int kVarRingP5 = 128 | (3 << 8);
 constexpr int kVarRingP4 = 128;
 constexpr int kVarSorted = 1 << 17; /* group the tile's keys by length (the SORT pipeline) */
+constexpr int kVarRingSorted = 128 | 16384; /* 256-key wave tiles hashed in length-sorted rounds (6 KiB slots) */
 
 int grid_cap()
 {
@@ -1763,6 +1810,18 @@ hipError_t launch_wr_x(const uint8_t *base, const uint64_t *off, uint64_t delta,
                        hipStream_t stream, int var)
 {
     const bool w4 = (var & 2048) != 0;
+    if (var & 16384) { /* 256-key tiles sorted by length, four rounds per wave */
+        switch ((var >> 8) & 7) {
+        case 1: return w4 ? launch_wr_plain<MODE, VAR, 8, 1, 2, 4, 256>(base, off, delta, nkeys, out, stream)
+                          : launch_wr_plain<MODE, VAR, 8, 1, 2, 1, 256>(base, off, delta, nkeys, out, stream);
+        case 3: return w4 ? launch_wr_plain<MODE, VAR, 6, 2, 3, 4, 256>(base, off, delta, nkeys, out, stream)
+                          : launch_wr_plain<MODE, VAR, 6, 2, 3, 1, 256>(base, off, delta, nkeys, out, stream);
+        case 7: return w4 ? launch_wr_plain<MODE, VAR, 5, 1, 2, 4, 256>(base, off, delta, nkeys, out, stream)
+                          : launch_wr_plain<MODE, VAR, 5, 1, 2, 1, 256>(base, off, delta, nkeys, out, stream);
+        default: return w4 ? launch_wr_plain<MODE, VAR, 6, 1, 2, 4, 256>(base, off, delta, nkeys, out, stream)
+                           : launch_wr_plain<MODE, VAR, 6, 1, 2, 1, 256>(base, off, delta, nkeys, out, stream);
+        }
+    }
     if (var & 8192) { /* 64-key tiles, one key per lane */
         switch ((var >> 8) & 7) {
         case 1: return w4 ? launch_wr_plain<MODE, VAR, 2, 1, 2, 4, 64>(base, off, delta, nkeys, out, stream)
@@ -1810,8 +1869,8 @@ hipError_t launch_wr_mode(const uint8_t *base, const uint64_t *off, uint64_t del
                           hipStream_t stream, int var)
 {
     if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_MD5) {
-        if (var & (2048 | 4096 | 8192)) {
-            if (var & 4096) return launch_wr_x<MODE, 512>(base, off, delta, nkeys, out, stream, var);
+        if (var & (2048 | 4096 | 8192 | 16384)) {
+            if ((var & 4096) && !(var & 16384)) return launch_wr_x<MODE, 512>(base, off, delta, nkeys, out, stream, var);
             return launch_wr_x<MODE, 0>(base, off, delta, nkeys, out, stream, var);
         }
         if (var & 8) { /* DIAGNOSTIC no-hash build: default and P5 ring shapes only */
@@ -1916,7 +1975,12 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
     if (fixed && mean < 20u) return kVarWorkgroup;
     /* varying lengths: md5 and the crcs gain from length-grouped waves
      * (md5: a wave runs a second block if any lane needs one) */
-    if (mode == NC_GPUHASH_MD5) return mean < 28u ? (kVarWorkgroup | kVarSorted) : (kVarRegStaged | kVarSorted);
+    if (mode == NC_GPUHASH_MD5) {
+        /* short varying keys: the wave ring's in-wave length sort (a 256-key
+         * tile of ~19 B keys fits its 6 KiB slot); longer ones: grouped tiles */
+        if (mean < 22u) return kVarRingSorted;
+        return mean < 28u ? (kVarWorkgroup | kVarSorted) : (kVarRegStaged | kVarSorted);
+    }
     if (crc && mean < 28u) return kVarWorkgroup | kVarSorted;
     return kVarRegStaged;
 }
