@@ -281,3 +281,21 @@ def test_key_buffers_beyond_4gib(gpu):
             assert int(g[i]) == p % 4, (shape, i)
     del kd, od, out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("var", [16512, 16512 | 2048 | 768, 16512 | 1792, 128, 2176, 10624])
+def test_wave_ring_ragged_tiles(gpu, oracle, var):
+    """Wave-ring shapes (incl. 256-key length-sorted rounds) on batch sizes
+    around their 64/128/256-key tiles, Zipf keys, misaligned key buffer,
+    against the oracle (fnv1a_64 and md5 take every shape, the other modes the
+    plain ring)."""
+    L.lib().nc_gpuhash_set_tuning(0, 0, var)
+    try:
+        for n in (1, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 513, 1025, 4097):
+            keys, off = t.synth_host(t.SynthSpec.zipf(60 + n % 7), 3, n)
+            kd, od = to_dev(keys, off, shift=5)
+            for m in (1, 6, 3, 10):
+                np.testing.assert_array_equal(gpu_hash(m, kd, od), oracle.batch(m, keys, off),
+                                              err_msg=f"var={var} n={n} mode={m}")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
