@@ -218,6 +218,7 @@ rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const u
  * wave-ring options (fnv1a_64, md5: 4 waves per workgroup, pair-interleaved
  * keys, 64-key tiles, 256-key tiles hashed in length-sorted rounds); bit 16: the plain workgroup
  * pipeline as an explicit choice; bit 17: length-grouped tiles, as sort = 1;
+ * bit 18: workgroup pipelines launch three resident sets of workgroups;
  * -1 = keep). */
 rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 

@@ -40,14 +40,15 @@ def gpu_hash(mode, keys_d, off_d):
                         (0, 0, 1 << 17), (0, 0, 32), (0, 1, 32), (11, 1, 33), (9, 0, 32), (0, 0, 64), (0, 1, 64),
                         (0, 0, 96), (7, 1, 96), (0, 0, 128), (37, 0, 129), (0, 0, 384), (5, 0, 640),
                         (0, 0, 896), (0, 0, 192), (0, 0, 2432 | 4096), (3, 0, 3968 | 4096), (0, 0, 2176),
-                        (0, 0, 10624), (0, 0, 16512), (7, 0, 16512 | 2048 | 768), (0, 0, 16512 | 1792)],
+                        (0, 0, 10624), (0, 0, 16512), (7, 0, 16512 | 2048 | 768), (0, 0, 16512 | 1792),
+                        (0, 0, 65536 | (1 << 18)), (0, 1, 32 | (1 << 18))],
                 ids=["persistent+sort", "auto", "workgroup", "grid37+sort+shiftadd", "shiftadd", "grid5+sort",
                      "sorted_bit", "regstage", "regstage+sort", "grid11+regstage+sort+shiftadd", "grid9+regstage",
                      "cached", "cached+sort", "regstage+cached", "grid7+regstage+cached+sort", "wavering",
                      "grid37+wavering+shiftadd", "wavering_4_1_2", "grid5+wavering_4_3_5", "wavering_5_2_3",
                      "wavering+cached", "wavering_w4_pair", "grid3+wavering_3_1_2_w4_pair", "wavering_w4",
                      "wavering_t64_w4", "wavering_t256_sorted", "grid7+wavering_t256_sorted_w4_6_2_3",
-                     "wavering_t256_sorted_5_1_2"])
+                     "wavering_t256_sorted_5_1_2", "workgroup_over3", "regstage+sort+over3"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)

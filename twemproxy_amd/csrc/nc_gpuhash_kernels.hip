@@ -1665,6 +1665,7 @@ constexpr int kVarRingP5 = 128 | (3 << 8);
 constexpr int kVarRingP4 = 128;
 constexpr int kVarSorted = 1 << 17; /* group the tile's keys by length (the SORT pipeline) */
 constexpr int kVarRingSorted = 128 | 16384; /* 256-key wave tiles hashed in length-sorted rounds (6 KiB slots) */
+constexpr int kVarOver = 1 << 18; /* workgroup pipelines: three resident sets of workgroups per launch */
 
 int grid_cap()
 {
@@ -1699,7 +1700,7 @@ int num_cus()
 
 template <int MODE, bool SORT, int VAR>
 hipError_t launch_kernel(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
-                         hipStream_t stream)
+                         hipStream_t stream, int var)
 {
     /* persistent grid: every resident workgroup slot once (occupancy query
      * cached per instantiation), unless a cap is set */
@@ -1714,7 +1715,12 @@ hipError_t launch_kernel(const uint8_t *base, const uint64_t *off, uint64_t delt
     }
     const uint64_t ntiles = (nkeys + kTile - 1) / kTile;
     const int cap = grid_cap();
-    uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu;
+    /* kVarOver: three resident sets of workgroups instead of one. The grid
+     * stride still walks every tile, but workgroups whose keys ran short
+     * finish early and new ones fill their slots: with varying key lengths
+     * (Zipf) this balances the CUs (C2 fnv1a_64: 0.49 -> 0.45 ms). */
+    const uint64_t over = (var & kVarOver) ? 3u : 1u;
+    uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu * over;
     if (grid > ntiles) grid = ntiles;
     (void)hipGetLastError(); /* a stale error from another library's call must not be reported as ours */
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, stream, base, off, delta, nkeys, out, ntiles);
@@ -1734,28 +1740,28 @@ hipError_t launch_sorted(const uint8_t *base, const uint64_t *off, uint64_t delt
     if constexpr (MODE == NC_GPUHASH_FNV1A_64 && !SORT) {
         if (var & 8) {
             switch (var & 6) {
-            case 2: return launch_kernel<MODE, SORT, 10>(base, off, delta, nkeys, out, stream);
-            case 4: return launch_kernel<MODE, SORT, 12>(base, off, delta, nkeys, out, stream);
-            case 6: return launch_kernel<MODE, SORT, 14>(base, off, delta, nkeys, out, stream);
-            default: return launch_kernel<MODE, SORT, 8>(base, off, delta, nkeys, out, stream);
+            case 2: return launch_kernel<MODE, SORT, 10>(base, off, delta, nkeys, out, stream, var);
+            case 4: return launch_kernel<MODE, SORT, 12>(base, off, delta, nkeys, out, stream, var);
+            case 6: return launch_kernel<MODE, SORT, 14>(base, off, delta, nkeys, out, stream, var);
+            default: return launch_kernel<MODE, SORT, 8>(base, off, delta, nkeys, out, stream, var);
             }
         }
-        if (var & 16) return launch_kernel<MODE, SORT, 16>(base, off, delta, nkeys, out, stream);
+        if (var & 16) return launch_kernel<MODE, SORT, 16>(base, off, delta, nkeys, out, stream, var);
     }
     if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_MD5) {
-        if (var & 64) return (var & 32) ? launch_kernel<MODE, SORT, 32 | 64>(base, off, delta, nkeys, out, stream)
-                                        : launch_kernel<MODE, SORT, 64>(base, off, delta, nkeys, out, stream);
+        if (var & 64) return (var & 32) ? launch_kernel<MODE, SORT, 32 | 64>(base, off, delta, nkeys, out, stream, var)
+                                        : launch_kernel<MODE, SORT, 64>(base, off, delta, nkeys, out, stream, var);
     }
     if (var & 32) {
         if constexpr (has_mul_variant(MODE)) {
-            if (var & 1) return launch_kernel<MODE, SORT, 33>(base, off, delta, nkeys, out, stream);
+            if (var & 1) return launch_kernel<MODE, SORT, 33>(base, off, delta, nkeys, out, stream, var);
         }
-        return launch_kernel<MODE, SORT, 32>(base, off, delta, nkeys, out, stream);
+        return launch_kernel<MODE, SORT, 32>(base, off, delta, nkeys, out, stream, var);
     }
     if constexpr (has_mul_variant(MODE)) {
-        if (var & 1) return launch_kernel<MODE, SORT, 1>(base, off, delta, nkeys, out, stream);
+        if (var & 1) return launch_kernel<MODE, SORT, 1>(base, off, delta, nkeys, out, stream, var);
     }
-    return launch_kernel<MODE, SORT, 0>(base, off, delta, nkeys, out, stream);
+    return launch_kernel<MODE, SORT, 0>(base, off, delta, nkeys, out, stream, var);
 }
 
 template <int MODE>
@@ -1963,25 +1969,31 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
     const bool crc = mode == NC_GPUHASH_CRC16 || mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A;
     const bool fnv_like = mode == NC_GPUHASH_FNV1_64 || mode == NC_GPUHASH_FNV1A_64 || mode == NC_GPUHASH_FNV1_32 ||
                           mode == NC_GPUHASH_FNV1A_32 || mode == NC_GPUHASH_HSIEH || mode == NC_GPUHASH_MURMUR;
+    const bool md5 = mode == NC_GPUHASH_MD5;
     if (mean >= 80u) { /* tiles overflow the workgroup slab: wave ring, deeper or wider slab slots */
-        if (mode == NC_GPUHASH_MD5) return mean >= 192u ? kVarRingP5 : kVarWorkgroup;
+        if (md5) return mean >= 192u ? kVarRingP5 : kVarWorkgroup;
         if (mode == NC_GPUHASH_ONE_AT_A_TIME || mode == NC_GPUHASH_HSIEH) return kVarRingP5;
         return kVarRingP4;
     }
-    if (fixed && mean >= 20u && mean <= 40u) {
-        if (fnv_like) return kVarRingP5;
-        return crc ? kVarWorkgroup : kVarRegStaged;
+    if (fixed) {
+        if (mean >= 20u && mean <= 40u) { /* C3 */
+            if (fnv_like) return kVarRingP5;
+            if (crc) return kVarWorkgroup | kVarOver;
+            return md5 ? (kVarRegStaged | kVarOver) : kVarRegStaged;
+        }
+        if (mean < 20u) return md5 ? (kVarWorkgroup | kVarOver) : kVarWorkgroup;
+        return kVarRegStaged;
     }
-    if (fixed && mean < 20u) return kVarWorkgroup;
-    /* varying lengths: md5 and the crcs gain from length-grouped waves
-     * (md5: a wave runs a second block if any lane needs one) */
-    if (mode == NC_GPUHASH_MD5) {
-        /* short varying keys: the wave ring's in-wave length sort (a 256-key
-         * tile of ~19 B keys fits its 6 KiB slot); longer ones: grouped tiles */
-        if (mean < 22u) return kVarRingSorted;
-        return mean < 28u ? (kVarWorkgroup | kVarSorted) : (kVarRegStaged | kVarSorted);
+    /* varying lengths: a wave runs as long as its longest key (a second md5
+     * block if any lane needs one); length-grouped tiles and oversubscribed
+     * grids rebalance that */
+    if (mean < 22u) { /* C2 */
+        if (md5) return kVarRingSorted;
+        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarWorkgroup | kVarSorted | kVarOver;
+        return kVarWorkgroup | kVarOver;
     }
-    if (crc && mean < 28u) return kVarWorkgroup | kVarSorted;
+    if (md5) return mean < 28u ? (kVarWorkgroup | kVarSorted | kVarOver) : (kVarRegStaged | kVarSorted);
+    if (crc || mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarRegStaged | kVarOver;
     return kVarRegStaged;
 }
 
@@ -1993,7 +2005,7 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
     const uint64_t delta = (uint64_t)(kp & 15u);
     int var = g_variant != 0 ? g_variant : pick_variant(mode, nkeys, shape);
     const bool sort = sort_enabled() || (var & kVarSorted) != 0;
-    var &= ~(kVarWorkgroup | kVarSorted);
+    var &= ~(kVarWorkgroup | kVarSorted); /* kVarOver rides along to launch_kernel */
     /* the wave ring DMAs offsets 16 bytes per lane: it needs 16-byte aligned
      * offsets (any other alignment takes the workgroup pipeline) */
     if ((var & 128) != 0 && (reinterpret_cast<uintptr_t>(d_off) & 15u) != 0) var = g_variant != 0 ? 0 : 32;
