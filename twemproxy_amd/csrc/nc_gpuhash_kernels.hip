@@ -1809,8 +1809,10 @@ hipError_t launch_wr_plain(const uint8_t *base, const uint64_t *off, uint64_t de
                                                                wr_lds_fixed<MODE, kDistNone, P, DS, DO, WPW, TK>());
 }
 
-/* EXPERIMENT (fnv1a_64 only): bit 11 = four waves per workgroup (one per
- * SIMD), bit 12 = pair-interleaved hashing, bit 0 = shift-add multiply */
+/* Wave-ring options, built for fnv1a_64 and md5 only: bit 11 = four waves per
+ * workgroup (one per SIMD), bit 12 = pair-interleaved hashing, bit 13 =
+ * 64-key tiles, bit 14 = 256-key tiles hashed in length-sorted rounds (the
+ * shape policy's md5 choice for short varying keys); bits 8-10 the shape */
 template <int MODE, int VAR>
 hipError_t launch_wr_x(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                        hipStream_t stream, int var)
