@@ -163,7 +163,7 @@ def test_auto_policy_choices():
     assert t.pick_variant("md5", n, (16 * n, 16, 16)) == WG | OVER
     assert t.pick_variant("crc32", n >> 3, (256 * (n >> 3), 256, 256)) == RING4
     assert t.pick_variant("md5", n >> 3, (256 * (n >> 3), 256, 256)) == RING5
-    assert t.pick_variant("md5", n >> 3, (128 * (n >> 3), 128, 128)) == WG
+    assert t.pick_variant("md5", n >> 3, (128 * (n >> 3), 128, 128)) == WG | OVER
     assert t.pick_variant("hsieh", 1000, (100000, 100, 100)) == RING5
     assert t.pick_variant("fnv1a_64", 0, (0, 0, 0)) == RS
     assert L.lib().nc_gpuhash_pick_variant(12, n, None) == -1

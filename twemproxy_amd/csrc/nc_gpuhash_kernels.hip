@@ -1973,7 +1973,7 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
                           mode == NC_GPUHASH_FNV1A_32 || mode == NC_GPUHASH_HSIEH || mode == NC_GPUHASH_MURMUR;
     const bool md5 = mode == NC_GPUHASH_MD5;
     if (mean >= 80u) { /* tiles overflow the workgroup slab: wave ring, deeper or wider slab slots */
-        if (md5) return mean >= 192u ? kVarRingP5 : kVarWorkgroup;
+        if (md5) return mean >= 192u ? kVarRingP5 : (kVarWorkgroup | kVarOver);
         if (mode == NC_GPUHASH_ONE_AT_A_TIME || mode == NC_GPUHASH_HSIEH) return kVarRingP5;
         return kVarRingP4;
     }
