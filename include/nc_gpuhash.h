@@ -214,9 +214,10 @@ rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const u
  * for fixed 32-byte keys, fnv1a_64 unsorted only; bit 5: register-staged
  * pipeline, two tiles in flight; bit 6: default cache policy on the key,
  * offset and output streams instead of non-temporal, fnv1a_64 and md5 only;
- * bit 7: wave-ring pipeline, bits 8-10 its slab/look-ahead shape; bits 11-13:
+ * bit 7: wave-ring pipeline, bits 8-10 its slab/look-ahead shape; bits 11-15:
  * wave-ring options (fnv1a_64, md5: 4 waves per workgroup, pair-interleaved
- * keys, 64-key tiles, 256-key tiles hashed in length-sorted rounds); bit 16: the plain workgroup
+ * keys, 64-key tiles, 256-key tiles hashed in length-sorted rounds, 128-key
+ * tiles in two sorted rounds); bit 16: the plain workgroup
  * pipeline as an explicit choice; bit 17: length-grouped tiles, as sort = 1;
  * bit 18: workgroup pipelines launch three resident sets of workgroups;
  * -1 = keep). */

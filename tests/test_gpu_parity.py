@@ -284,7 +284,7 @@ def test_key_buffers_beyond_4gib(gpu):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("var", [16512, 16512 | 2048 | 768, 16512 | 1792, 128, 2176, 10624])
+@pytest.mark.parametrize("var", [16512, 16512 | 2048 | 768, 16512 | 1792, 128, 2176, 10624, 32896, 32896 | 2048])
 def test_wave_ring_ragged_tiles(gpu, oracle, var):
     """Wave-ring shapes (incl. 256-key length-sorted rounds) on batch sizes
     around their 64/128/256-key tiles, Zipf keys, misaligned key buffer,

@@ -1203,7 +1203,7 @@ struct WrDist {
  * wave and hashes them in four rounds of 64 similar lengths: a round runs as
  * long as its longest key, so Zipf lengths cost ~the sum of the four quartile
  * maxima instead of four times the tile maximum. */
-template <int P, int DS, int DO, int TK = kWrTile>
+template <int P, int DS, int DO, int TK = kWrTile, bool SR = (TK == 256)>
 struct WrRing {
     static_assert(DO > DS && DS >= 1 && DO >= 2 * DS - 1, "offsets must run far enough ahead of slabs");
     static_assert(TK == 64 || TK == 128 || TK == 256, "a wave tile is one, two or four keys per lane");
@@ -1216,8 +1216,8 @@ struct WrRing {
     static constexpr uint32_t kSlot = (uint32_t)P * 1024u;
     static constexpr uint32_t kOffOffs = NS * kSlot;  /* slab over-reads land in the next slot / the offsets */
     static constexpr uint32_t kOffDump = kOffOffs + NO * kOffSlot;
-    static constexpr uint32_t kSortOffs = kOffDump + 16u; /* TK 256: u32 hist[64] + u32 order[256] */
-    static constexpr uint32_t kBytes = kSortOffs + (TK == 256 ? 4u * (64u + 256u) : 0u);
+    static constexpr uint32_t kSortOffs = kOffDump + 16u; /* sorted rounds: u32 hist[64] + u32 order[TK] */
+    static constexpr uint32_t kBytes = kSortOffs + (SR ? 4u * (64u + (uint32_t)TK) : 0u);
     static constexpr int kWaitOff = (DO - DS) * kIter;
     static constexpr int kWaitSlab = DS * kIter;
     static_assert(kWaitSlab <= 63 && kWaitOff <= 63, "vmcnt is 6 bits");
@@ -1378,10 +1378,18 @@ __device__ __forceinline__ uint32_t key_value(const Src &src, typename Src::pos_
     }
 }
 
-template <int MODE, int DIST, int P, int DS, int DO, int WPW, int TK = kWrTile>
+/* VAR bit 2 on the wave ring: hash the tile in length-sorted rounds (always
+ * for 256-key tiles) */
+template <int VAR, int TK>
+constexpr bool wr_sorted()
+{
+    return TK == 256 || (VAR & 4) != 0;
+}
+
+template <int MODE, int DIST, int P, int DS, int DO, int WPW, int TK = kWrTile, int VAR = 0>
 constexpr uint32_t wr_lds_fixed()
 {
-    return (uint32_t)WPW * WrRing<P, DS, DO, TK>::kBytes + (uses_crc_table<MODE>() ? 1024u : 0u);
+    return (uint32_t)WPW * WrRing<P, DS, DO, TK, wr_sorted<VAR, TK>()>::kBytes + (uses_crc_table<MODE>() ? 1024u : 0u);
 }
 
 template <int MODE, int VAR, int P, int DS, int DO, int DIST, int WPW, int TK = kWrTile>
@@ -1390,12 +1398,13 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
                                                               uint64_t nkeys, uint32_t *__restrict__ out,
                                                               uint64_t ntiles, WrDist dist)
 {
-    using R = WrRing<P, DS, DO, TK>;
+    constexpr bool kSortRounds = wr_sorted<VAR, TK>();
+    using R = WrRing<P, DS, DO, TK, kSortRounds>;
     constexpr uint32_t NS = R::NS, NO = R::NO;
     constexpr uint32_t kWrOffSlot = R::kOffSlot;
     constexpr bool kNT = (VAR & 64) == 0;
     constexpr uint32_t kTabOffs = (uint32_t)WPW * R::kBytes;
-    constexpr uint32_t kContOffs = wr_lds_fixed<MODE, DIST, P, DS, DO, WPW, TK>();
+    constexpr uint32_t kContOffs = wr_lds_fixed<MODE, DIST, P, DS, DO, WPW, TK, VAR>();
     extern __shared__ __attribute__((aligned(16))) uint8_t wr_lds[];
 
     const uint32_t t = threadIdx.x;
@@ -1540,16 +1549,16 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
                 goto stores;
             }
         }
-        if constexpr (TK == 256) {
-            /* counting sort of the tile's 256 keys by length class, in LDS:
-             * one wave, so its LDS operations retire in order */
+        if constexpr (kSortRounds) {
+            /* counting sort of the tile's keys by length class, in LDS: one
+             * wave, so its LDS operations retire in order */
             uint32_t *hist = reinterpret_cast<uint32_t *>(smem + R::kSortOffs);
             uint32_t *order = hist + 64;
-            uint32_t bk[4], rk[4];
+            uint32_t bk[R::NST], rk[R::NST];
             hist[lane] = 0u;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
+            for (int q = 0; q < R::NST; q++) {
                 const uint32_t i = key_of[q];
                 const uint32_t ie = i + 1u >= cnt ? (uint32_t)TK : i + 1u;
                 const uint32_t len = i < cnt ? ob[2u * ie] - ob[2u * i] : 0u;
@@ -1567,10 +1576,10 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
             hist[lane] = incl - c; /* first rank of length class `lane` */
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-            for (int q = 0; q < 4; q++) order[hist[bk[q]] + rk[q]] = key_of[q];
+            for (int q = 0; q < R::NST; q++) order[hist[bk[q]] + rk[q]] = key_of[q];
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-            for (int q = 0; q < 4; q++) key_of[q] = order[64u * (uint32_t)q + lane];
+            for (int q = 0; q < R::NST; q++) key_of[q] = order[64u * (uint32_t)q + lane];
         }
 #pragma unroll
         for (int q = 0; q < R::NST; q++) {
@@ -1806,18 +1815,22 @@ hipError_t launch_wr_plain(const uint8_t *base, const uint64_t *off, uint64_t de
 {
     const WrDist none{nullptr, 0u, 0u};
     return launch_wr<MODE, VAR, P, DS, DO, kDistNone, WPW, TK>(base, off, delta, nkeys, out, stream, none,
-                                                               wr_lds_fixed<MODE, kDistNone, P, DS, DO, WPW, TK>());
+                                                               wr_lds_fixed<MODE, kDistNone, P, DS, DO, WPW, TK, VAR>());
 }
 
 /* Wave-ring options, built for fnv1a_64 and md5 only: bit 11 = four waves per
  * workgroup (one per SIMD), bit 12 = pair-interleaved hashing, bit 13 =
  * 64-key tiles, bit 14 = 256-key tiles hashed in length-sorted rounds (the
- * shape policy's md5 choice for short varying keys); bits 8-10 the shape */
+ * shape policy's md5 choice for short varying keys), bit 15 = 128-key tiles
+ * in two sorted rounds; bits 8-10 the shape */
 template <int MODE, int VAR>
 hipError_t launch_wr_x(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                        hipStream_t stream, int var)
 {
     const bool w4 = (var & 2048) != 0;
+    if (var & 32768) /* 128-key tiles in two length-sorted rounds, 3 KiB slots (ties the workgroup x3 on C2) */
+        return w4 ? launch_wr_plain<MODE, VAR | 4, 3, 1, 2, 4>(base, off, delta, nkeys, out, stream)
+                  : launch_wr_plain<MODE, VAR | 4, 3, 1, 2, 1>(base, off, delta, nkeys, out, stream);
     if (var & 16384) { /* 256-key tiles sorted by length, four rounds per wave */
         switch ((var >> 8) & 7) {
         case 1: return w4 ? launch_wr_plain<MODE, VAR, 8, 1, 2, 4, 256>(base, off, delta, nkeys, out, stream)
@@ -1877,7 +1890,7 @@ hipError_t launch_wr_mode(const uint8_t *base, const uint64_t *off, uint64_t del
                           hipStream_t stream, int var)
 {
     if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_MD5) {
-        if (var & (2048 | 4096 | 8192 | 16384)) {
+        if (var & (2048 | 4096 | 8192 | 16384 | 32768)) {
             if ((var & 4096) && !(var & 16384)) return launch_wr_x<MODE, 512>(base, off, delta, nkeys, out, stream, var);
             return launch_wr_x<MODE, 0>(base, off, delta, nkeys, out, stream, var);
         }
