@@ -126,6 +126,14 @@ def roofline(alg_bytes: float, kern_ms: float, traffic):
     return r
 
 
+def read_ceiling(t, rf, buf):
+    """Same-run STREAM-style read ceiling over the key buffer:
+    the achievable HBM read rate on this box, after the timed region."""
+    probe = t.probe_read_gbs(buf, 20)
+    rf["read_ceiling_gbs"] = round(probe, 1)
+    rf["frac_of_read_ceiling"] = round(rf["achieved"] / probe, 4)
+
+
 def load_traffic(kernel_mode: str, workload: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this
     workload (profiles/pmc_*.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950
@@ -236,6 +244,7 @@ def main():
     value = total_keys / wall / 1e6
     alg = key_bytes + 12.0 * nk  # key bytes + u64 offset + u32 hash per key
     rf = roofline(alg, kern_ms, load_traffic("fnv1a_64", "C2"))
+    read_ceiling(t, rf, keys)
 
     res = {
         "metric": METRIC, "value": round(value, 1), "unit": "Mkeys/s", "n_gpus": world,
@@ -290,6 +299,7 @@ def main():
             "value": round(sum_over_ranks(torch, float(n_local), dist_on) * args.steps / w3 / 1e6, 1),
             "unit": "Mkeys/s", "kernel_ms": round(k3, 4),
             "roofline": roofline(kb3 + 12.0 * n_local, k3, load_traffic("fnv1a_64", "C3"))}
+        read_ceiling(t, res["c3_fnv1a_64"]["roofline"], keys3)
         del keys3, off3, out3
 
     # ---- CPU baseline (rank 0, N = 1)
