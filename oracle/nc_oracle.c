@@ -645,3 +645,199 @@ int oracle_mc_parse(const uint8_t *s, uint64_t n, uint64_t max_keys, uint64_t *k
     *consumed = done;
     return 0;
 }
+
+/*
+ * redis_parse_req (src/proto/nc_redis.c:460-1900) for a stream of pipelined
+ * RESP requests, one byte at a time through the reference's states, for the
+ * command classes whose keys the device extracts:
+ *   arg0  redis_arg0 (:64-104, less AUTH, which the proxy answers itself),
+ *   arg1  redis_arg1 (:106-140), argn redis_argn (:208-298),
+ *   argx  redis_argx (:300-319), argkvx redis_argkvx (:321-334).
+ * States: SW_START (:478-490), SW_NARG (:492-509), SW_NARG_LF (:511-521),
+ * SW_REQ_TYPE_LEN (:523-543; rlen 0 is an error), SW_REQ_TYPE (:557-1326;
+ * the name compares case-insensitively, nc_proto.h:87), SW_REQ_TYPE_LF
+ * (:1333-1360; narg 1 is an error for these classes), SW_KEY_LEN
+ * (:1362-1389; rlen >= mbuf_data_size() is an error, no digits is rlen 0),
+ * SW_KEY (:1403-1435, a key is rlen bytes then CR), SW_KEY_LF (:1437-1490),
+ * SW_ARG1_LEN (:1492-1512; no digits is an error), SW_ARG1 (:1526-1544),
+ * SW_ARG1_LF (:1546-1589), SW_ARGN_LEN/ARGN/ARGN_LF (:1807-1878).
+ * Lengths and counts accumulate in uint32_t like r->rlen / r->rnarg.
+ * Statuses: 0 ok, -1 syntax error, -2 key length >= the mbuf data size,
+ * -3 a command outside these classes (unknown to this table; the host parser
+ * decides). Stops at the first non-ok request (recorded) or at an incomplete
+ * last one (not recorded).
+ */
+enum { RC_NONE, RC_ARG0, RC_ARG1, RC_ARGN, RC_ARGX, RC_ARGKVX };
+
+static const char *const rc_arg0[] = {"persist", "pttl", "ttl", "type", "dump", "decr", "get", "getdel", "incr",
+                                      "strlen", "hgetall", "hkeys", "hlen", "hvals", "llen", "scard", "smembers",
+                                      "zcard", NULL};
+static const char *const rc_arg1[] = {"expire", "expireat", "pexpire", "pexpireat", "move", "append", "decrby",
+                                      "getbit", "getset", "incrby", "incrbyfloat", "setnx", "hexists", "hget",
+                                      "hstrlen", "lindex", "rpoplpush", "sismember", "zrank", "zrevrank", "zscore",
+                                      NULL};
+static const char *const rc_argn[] = {
+    "sort", "copy", "bitcount", "bitpos", "bitfield", "exists", "getex", "set", "hdel", "hmget", "hmset", "hscan",
+    "hset", "hrandfield", "lpush", "lpushx", "rpush", "rpushx", "lpop", "rpop", "lpos", "sadd", "sdiff",
+    "sdiffstore", "sinter", "sinterstore", "srem", "sunion", "sunionstore", "srandmember", "sscan", "spop",
+    "smismember", "pfadd", "pfmerge", "pfcount", "zadd", "zdiff", "zdiffstore", "zinter", "zinterstore", "zmscore",
+    "zpopmax", "zpopmin", "zrandmember", "zrange", "zrangebylex", "zrangebyscore", "zrangestore", "zrem",
+    "zrevrange", "zrevrangebylex", "zrevrangebyscore", "zscan", "zunion", "zunionstore", "geodist", "geopos",
+    "geohash", "geoadd", "georadius", "georadiusbymember", "geosearch", "geosearchstore", "restore", NULL};
+static const char *const rc_argx[] = {"mget", "del", "unlink", "touch", NULL};
+
+static int rc_in(const char *const *tab, const uint8_t *m, uint64_t len)
+{
+    for (; *tab; tab++) {
+        if (strlen(*tab) != len) continue;
+        uint64_t i = 0;
+        while (i < len && (m[i] == (uint8_t)(*tab)[i] || m[i] == (uint8_t)((*tab)[i] ^ 0x20))) i++;
+        if (i == len) return 1;
+    }
+    return 0;
+}
+
+int oracle_redis_class(const uint8_t *m, uint64_t len)
+{
+    if (rc_in(rc_arg0, m, len)) return RC_ARG0;
+    if (rc_in(rc_arg1, m, len)) return RC_ARG1;
+    if (rc_in(rc_argn, m, len)) return RC_ARGN;
+    if (rc_in(rc_argx, m, len)) return RC_ARGX;
+    if (len == 4 && rc_in((const char *const[]){"mset", NULL}, m, len)) return RC_ARGKVX;
+    return RC_NONE;
+}
+
+enum {
+    RS_START, RS_NARG, RS_NARG_LF, RS_TYPE_LEN, RS_TYPE_LEN_LF, RS_TYPE, RS_TYPE_LF, RS_KEY_LEN, RS_KEY_LEN_LF,
+    RS_KEY, RS_KEY_LF, RS_ARG_LEN, RS_ARG_LEN_LF, RS_ARG, RS_ARG_LF
+};
+
+int oracle_redis_parse(const uint8_t *s, uint64_t n, uint32_t max_key_len, uint64_t max_keys, uint64_t *kstart,
+                       uint32_t *klen, uint32_t *kreq, int32_t *status, uint64_t max_reqs, uint64_t *nkeys,
+                       uint64_t *nreqs_parsed, uint64_t *first_error, uint64_t *consumed)
+{
+    uint64_t nk = 0, nr = 0, done = 0, kn = 0, token = 0;
+    uint32_t narg = 0, rnarg = 0, rlen = 0;
+    int state = RS_START, cls = RC_NONE, have_token = 0, st = 0;
+    *first_error = UINT64_MAX;
+    for (uint64_t p = 0; p < n && st == 0; p++) {
+        const uint8_t ch = s[p];
+        int fin = 0;
+        switch (state) {
+        case RS_START:
+            if (ch != '*') { st = -1; break; }
+            rnarg = 0;
+            kn = 0;
+            state = RS_NARG;
+            break;
+        case RS_NARG:
+            if (ch >= '0' && ch <= '9') rnarg = rnarg * 10u + (uint32_t)(ch - '0');
+            else if (ch == '\r' && rnarg != 0) { narg = rnarg; state = RS_NARG_LF; }
+            else st = -1;
+            break;
+        case RS_NARG_LF:
+        case RS_TYPE_LEN_LF:
+        case RS_KEY_LEN_LF:
+        case RS_ARG_LEN_LF:
+            if (ch != '\n') { st = -1; break; }
+            state = state == RS_NARG_LF ? RS_TYPE_LEN : state == RS_TYPE_LEN_LF ? RS_TYPE
+                  : state == RS_KEY_LEN_LF ? RS_KEY : RS_ARG;
+            have_token = 0;
+            break;
+        case RS_TYPE_LEN:
+        case RS_KEY_LEN:
+        case RS_ARG_LEN:
+            if (!have_token) {
+                if (ch != '$') { st = -1; break; }
+                have_token = 1;
+                token = p;
+                rlen = 0;
+            } else if (ch >= '0' && ch <= '9') {
+                rlen = rlen * 10u + (uint32_t)(ch - '0');
+            } else if (ch == '\r') {
+                if (state == RS_TYPE_LEN && (rlen == 0 || rnarg == 0)) { st = -1; break; }
+                if (state == RS_KEY_LEN && rlen >= max_key_len) { st = -2; break; }
+                if (state == RS_KEY_LEN && rnarg == 0) { st = -1; break; }
+                if (state == RS_ARG_LEN && (p - token <= 1 || rnarg == 0)) { st = -1; break; }
+                rnarg--;
+                state = state == RS_TYPE_LEN ? RS_TYPE_LEN_LF : state == RS_KEY_LEN ? RS_KEY_LEN_LF : RS_ARG_LEN_LF;
+            } else {
+                st = -1;
+            }
+            break;
+        case RS_TYPE:
+        case RS_KEY:
+        case RS_ARG: {
+            /* rlen bytes of data, then CR: wait for the CR's byte to arrive */
+            const uint64_t m = p + rlen;
+            if (m >= n) { p = n; break; }
+            if (s[m] != '\r') { st = -1; break; }
+            if (state == RS_TYPE) {
+                cls = oracle_redis_class(s + p, rlen);
+                if (cls == RC_NONE) { st = -3; break; }
+                state = RS_TYPE_LF;
+            } else if (state == RS_KEY) {
+                if (nk + kn >= max_keys) return -1;
+                kstart[nk + kn] = p;
+                klen[nk + kn] = rlen;
+                kreq[nk + kn] = (uint32_t)nr;
+                kn++;
+                state = RS_KEY_LF;
+            } else {
+                state = RS_ARG_LF;
+            }
+            p = m;
+            break;
+        }
+        case RS_TYPE_LF:
+            if (ch != '\n' || narg == 1) { st = -1; break; }
+            state = RS_KEY_LEN;
+            have_token = 0;
+            break;
+        case RS_KEY_LF:
+            if (ch != '\n') { st = -1; break; }
+            have_token = 0;
+            if (cls == RC_ARG0) {
+                if (rnarg != 0) st = -1; else fin = 1;
+            } else if (cls == RC_ARG1) {
+                if (rnarg != 1) st = -1; else state = RS_ARG_LEN;
+            } else if (cls == RC_ARGN || cls == RC_ARGX) {
+                if (rnarg == 0) fin = 1; else state = cls == RC_ARGX ? RS_KEY_LEN : RS_ARG_LEN;
+            } else { /* argkvx */
+                if (narg % 2 == 0) st = -1; else state = RS_ARG_LEN;
+            }
+            break;
+        case RS_ARG_LF:
+            if (ch != '\n') { st = -1; break; }
+            have_token = 0;
+            if (cls == RC_ARG1) {
+                if (rnarg != 0) st = -1; else fin = 1;
+            } else if (cls == RC_ARGN) {
+                if (rnarg == 0) fin = 1; else state = RS_ARG_LEN; /* SW_ARG1_LF then SW_ARGN_LF: same rule */
+            } else { /* argkvx */
+                if (rnarg == 0) fin = 1; else state = RS_KEY_LEN;
+            }
+            break;
+        }
+        if (st != 0) break;
+        if (fin) {
+            if (nr >= max_reqs) return -1;
+            status[nr++] = 0;
+            nk += kn;
+            kn = 0;
+            done = p + 1;
+            state = RS_START;
+        }
+    }
+    if (st != 0) {
+        if (nr >= max_reqs) return -1;
+        status[nr] = st;
+        *first_error = nr;
+        nr++;
+    }
+    *nkeys = nk;
+    *nreqs_parsed = nr;
+    if (*first_error == UINT64_MAX) *first_error = nr;
+    *consumed = done;
+    return 0;
+}

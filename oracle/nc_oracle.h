@@ -95,6 +95,15 @@ int oracle_mc_parse(const uint8_t *s, uint64_t n, uint64_t max_keys, uint64_t *k
                     uint32_t *kreq, int32_t *status, uint64_t max_reqs, uint64_t *nkeys, uint64_t *nreqs_parsed,
                     uint64_t *first_error, uint64_t *consumed);
 
+/* redis_parse_req (src/proto/nc_redis.c) over a stream of RESP requests of
+ * the key classes arg0 / arg1 / argn / argx / argkvx, sequentially; see
+ * nc_oracle.c. max_key_len = mbuf_data_size(). 0, or -1 when a limit is hit. */
+int oracle_redis_parse(const uint8_t *s, uint64_t n, uint32_t max_key_len, uint64_t max_keys, uint64_t *kstart,
+                       uint32_t *klen, uint32_t *kreq, int32_t *status, uint64_t max_reqs, uint64_t *nkeys,
+                       uint64_t *nreqs_parsed, uint64_t *first_error, uint64_t *consumed);
+/* the key class of a command name (0 none, 1 arg0, 2 arg1, 3 argn, 4 argx, 5 argkvx) */
+int oracle_redis_class(const uint8_t *m, uint64_t len);
+
 #ifdef __cplusplus
 }
 #endif

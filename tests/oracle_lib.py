@@ -44,6 +44,13 @@ class Oracle:
         lib.oracle_mc_parse.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        lib.oracle_redis_parse.restype = ctypes.c_int
+        lib.oracle_redis_parse.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p]
+        lib.oracle_redis_class.restype = ctypes.c_int
+        lib.oracle_redis_class.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
         lib.oracle_ketama_build_live.restype = ctypes.c_int
         lib.oracle_ketama_build_live.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint32),
                                                  ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p, ctypes.c_uint32,
@@ -123,6 +130,27 @@ class Oracle:
         nk, nr = int(out[0]), int(out[1])
         info = {"nkeys": nk, "nparsed": nr, "first_error": int(out[2]), "consumed": int(out[3])}
         return ks[:nk], kl[:nk], kr[:nk], st[:nr], info
+
+    def redis_parse(self, stream: bytes, max_key_len: int = 16336, max_keys: int = 1 << 20,
+                    max_reqs: int = 1 << 20):
+        """RESP request stream -> (key starts, key lengths, key_req, statuses, info), like mc_parse."""
+        buf = np.frombuffer(stream, dtype=np.uint8) if len(stream) else np.zeros(1, np.uint8)
+        ks = np.zeros(max_keys, np.uint64)
+        kl = np.zeros(max_keys, np.uint32)
+        kr = np.zeros(max_keys, np.uint32)
+        st = np.zeros(max_reqs, np.int32)
+        out = (ctypes.c_uint64 * 4)()
+        rc = self.lib.oracle_redis_parse(buf.ctypes.data, len(stream), max_key_len, max_keys, ks.ctypes.data,
+                                         kl.ctypes.data, kr.ctypes.data, st.ctypes.data, max_reqs,
+                                         ctypes.byref(out, 0), ctypes.byref(out, 8), ctypes.byref(out, 16),
+                                         ctypes.byref(out, 24))
+        assert rc == 0
+        nk, nr = int(out[0]), int(out[1])
+        info = {"nkeys": nk, "nparsed": nr, "first_error": int(out[2]), "consumed": int(out[3])}
+        return ks[:nk], kl[:nk], kr[:nk], st[:nr], info
+
+    def redis_class(self, name: bytes) -> int:
+        return self.lib.oracle_redis_class(name, len(name))
 
     def modula_dispatch(self, idx: np.ndarray, h: int) -> int:
         return int(self.lib.oracle_modula_dispatch(idx.ctypes.data, idx.size, h))
