@@ -188,6 +188,41 @@ rstatus_t nc_gpuhash_mc_parse_device(nc_gpuhash_mc_parser_t *ps, const uint8_t *
                                      int32_t *d_req_status, struct nc_gpuhash_mc_result *result,
                                      void *stream);
 
+/* Key extraction on the device from pipelined redis (RESP) requests of the
+ * command classes whose keys redis_parse_req pushes (arg0 / arg1 / argn / argx
+ * / argkvx: src/proto/nc_redis.c:64-334, :460-1900; AUTH excluded). The
+ * boundaries of binary-safe requests are found by a speculative parse from
+ * every position after a CR LF, then the chain from byte 0 (pointer jumping).
+ * Keys are produced for the requests before the first one that fails or is of
+ * another command class; an incomplete last request is left for the next
+ * read, as the reference leaves it in the mbuf. */
+typedef struct nc_gpuhash_redis_parser nc_gpuhash_redis_parser_t;
+
+#define NC_GPUHASH_REDIS_OK            0
+#define NC_GPUHASH_REDIS_EINVAL       -1 /* syntax the reference rejects */
+#define NC_GPUHASH_REDIS_EKEYLEN      -2 /* key length >= mbuf_data_size() (nc_redis.c:1369-1375) */
+#define NC_GPUHASH_REDIS_EUNSUPPORTED -3 /* a command outside these classes: the host parser decides */
+
+struct nc_gpuhash_redis_result {
+    uint64_t nreqs;       /* requests parsed: the ok ones plus the failing one, if any */
+    uint64_t nkeys;       /* keys written (requests [0, first_error)) */
+    uint64_t first_error; /* index of the failing request, or nreqs */
+    uint64_t consumed;    /* stream bytes of requests [0, first_error) */
+};
+
+/* Device workspace for streams up to max_bytes (< 2^31), max_reqs requests and
+ * max_keys keys (each < 2^31). NULL with errno on failure. */
+nc_gpuhash_redis_parser_t *nc_gpuhash_redis_parser_create(uint64_t max_bytes, uint64_t max_reqs, uint64_t max_keys);
+void nc_gpuhash_redis_parser_destroy(nc_gpuhash_redis_parser_t *ps);
+
+/* Parse d_stream[0, nbytes); max_key_len is mbuf_data_size() (keys must be
+ * shorter). Outputs as nc_gpuhash_mc_parse_device, with NC_GPUHASH_REDIS_*
+ * statuses. Blocks until done. */
+rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps, const uint8_t *d_stream, uint64_t nbytes,
+                                        uint32_t max_key_len, uint8_t *d_keys, uint64_t *d_offsets,
+                                        uint32_t *d_key_req, int32_t *d_req_status,
+                                        struct nc_gpuhash_redis_result *result, void *stream);
+
 /* The launch variant the auto policy picks for this mode and shape (the
  * variant bits of nc_gpuhash_set_tuning; bit 16 = the plain workgroup
  * pipeline); -1 with errno EINVAL for an invalid mode. */

@@ -204,3 +204,12 @@ def test_mc_parser_argument_errors():
         assert not lib.nc_gpuhash_mc_parser_create(*args)
         assert ctypes.get_errno() == errno.EINVAL
     assert lib.nc_gpuhash_mc_parse_device(None, None, 0, None, None, None, None, None, None) == L.NC_ERROR
+
+
+def test_redis_parser_argument_errors():
+    lib = L.lib()
+    for args in ((0, 1, 1), (1, 0, 1), (1, 1, 0), (1 << 31, 1, 1), (1, 1 << 31, 1), (1, 1, 1 << 31)):
+        ctypes.set_errno(0)
+        assert not lib.nc_gpuhash_redis_parser_create(*args)
+        assert ctypes.get_errno() == errno.EINVAL
+    assert lib.nc_gpuhash_redis_parse_device(None, None, 0, 16336, None, None, None, None, None, None) == L.NC_ERROR

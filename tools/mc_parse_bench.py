@@ -2,7 +2,9 @@
 """Device key extraction (nc_gpuhash_mc_parse_device) on pipelined GET
 streams: C5's batch (64 connections x 128 pipelined "get <key>\\r\\n", C2
 Zipf printable keys) and a 2^22-request stream for throughput, then the
-extracted keys through fnv1a_64 and the fused server_idx. Prints JSON lines."""
+extracted keys through fnv1a_64 and the fused server_idx. Then the redis
+parser (nc_gpuhash_redis_parse_device) on the same keys as RESP GETs and on a
+mixed binary-safe pipeline (tests/redis_gen.py). Prints JSON lines."""
 import json
 import os
 import sys
@@ -66,5 +68,60 @@ def main():
                               "sample_hash_mismatches": bad}), flush=True)
 
 
+def resp_get_stream(t, np, nreq, seed=5):
+    """RESP "*2 $3 get $<len> <key>" x nreq over the same C5 keys"""
+    spec = t.SynthSpec.zipf(seed, charset=t.BYTES_PRINTABLE)
+    kh, oh = t.synth_host(spec, 0, nreq)
+    kb = kh.tobytes()
+    parts = []
+    for i in range(nreq):
+        k = kb[int(oh[i]): int(oh[i + 1])]
+        parts.append(b"*2\r\n$3\r\nget\r\n$%d\r\n%s\r\n" % (len(k), k))
+    return np.frombuffer(b"".join(parts), np.uint8).copy(), int(oh[-1])
+
+
+def timed(torch, ps, sd, reps):
+    for _ in range(3):
+        ps.parse(sd)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = ps.parse(sd)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps, out
+
+
+def redis_main():
+    import numpy as np
+    import torch
+
+    import twemproxy_amd as t
+    from tests import redis_gen as G
+
+    with t.RedisParser(max_bytes=1 << 30, max_reqs=1 << 23, max_keys=1 << 23) as ps:
+        for nreq in (64 * 128, 1 << 21):
+            buf, kbytes = resp_get_stream(t, np, nreq)
+            sd = torch.from_numpy(buf).cuda()
+            dt, (keys, off, kreq, status, info) = timed(torch, ps, sd, 20 if nreq < 100000 else 5)
+            assert info["nkeys"] == nreq and info["first_error"] == nreq
+            print(json.dumps({"workload": f"redis: {nreq} pipelined RESP GETs (C5 keys)",
+                              "stream_bytes": int(buf.size), "key_bytes": kbytes,
+                              "parse_ms_wall": round(dt * 1e3, 4),
+                              "stream_gb_s": round(buf.size / dt / 1e9, 2), "mreq_s": round(nreq / dt / 1e6, 1)}),
+                  flush=True)
+        rng = np.random.default_rng(1)
+        b, reqs = G.stream(rng, 200_000)
+        sd = torch.from_numpy(np.frombuffer(b, np.uint8).copy()).cuda()
+        dt, (keys, off, kreq, status, info) = timed(torch, ps, sd, 5)
+        assert info["nreqs"] == len(reqs) and info["consumed"] == len(b)
+        print(json.dumps({"workload": "redis: 200000 mixed binary-safe requests (tests/redis_gen.py, seed 1)",
+                          "stream_bytes": len(b), "nkeys": info["nkeys"], "parse_ms_wall": round(dt * 1e3, 4),
+                          "stream_gb_s": round(len(b) / dt / 1e9, 2), "mreq_s": round(len(reqs) / dt / 1e6, 1)}),
+              flush=True)
+
+
 if __name__ == "__main__":
+    if "--redis" in sys.argv:
+        redis_main()
+        sys.exit(0)
     main()

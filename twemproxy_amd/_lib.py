@@ -49,6 +49,13 @@ class NcMcResult(ctypes.Structure):
                 ("consumed", ctypes.c_uint64)]
 
 
+class NcRedisResult(ctypes.Structure):
+    """struct nc_gpuhash_redis_result (include/nc_gpuhash.h)."""
+
+    _fields_ = [("nreqs", ctypes.c_uint64), ("nkeys", ctypes.c_uint64), ("first_error", ctypes.c_uint64),
+                ("consumed", ctypes.c_uint64)]
+
+
 class NcKeySpan(ctypes.Structure):
     """struct nc_keyspan — the shape of twemproxy's struct keypos (src/nc_message.h:232-235)."""
 
@@ -99,6 +106,13 @@ SIGNATURES = {
     ),
     "nc_gpuhash_mc_parser_create": (ctypes.c_void_p, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
     "nc_gpuhash_mc_parser_destroy": (None, [ctypes.c_void_p]),
+    "nc_gpuhash_redis_parser_create": (ctypes.c_void_p, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
+    "nc_gpuhash_redis_parser_destroy": (None, [ctypes.c_void_p]),
+    "nc_gpuhash_redis_parse_device": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(NcRedisResult), ctypes.c_void_p],
+    ),
     "nc_gpuhash_mc_parse_device": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

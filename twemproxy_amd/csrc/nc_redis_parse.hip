@@ -1,0 +1,522 @@
+/*
+ * Key extraction on the device for redis: a stream of
+ * pipelined RESP requests into the key CSR the hash kernels take, plus the
+ * request each key belongs to.
+ *
+ * Reference: redis_parse_req, /root/reference/src/proto/nc_redis.c:460-1900,
+ * for the command classes whose keys it pushes one by one:
+ *   arg0 redis_arg0 (:64-104, less AUTH), arg1 redis_arg1 (:106-140),
+ *   argn redis_argn (:208-298), argx redis_argx (:300-319),
+ *   argkvx redis_argkvx (:321-334).
+ * States: SW_START (:478-490), SW_NARG (:492-509), SW_NARG_LF (:511-521),
+ * SW_REQ_TYPE_LEN (:523-543), SW_REQ_TYPE (:557-1326), SW_REQ_TYPE_LF
+ * (:1333-1360), SW_KEY_LEN (:1362-1389), SW_KEY (:1403-1435), SW_KEY_LF
+ * (:1437-1490), SW_ARG1_LEN/ARG1/ARG1_LF (:1492-1589), SW_ARGN_* (:1807-1878).
+ * The oracle's sequential restatement is oracle/nc_oracle.c:oracle_redis_parse;
+ * statuses are the same (0 ok, -1 syntax, -2 key length >= mbuf data size,
+ * -3 a command outside these classes: the host parser takes over).
+ *
+ * RESP requests are length-prefixed and binary-safe, so request boundaries are
+ * not visible in the bytes. The device parses speculatively:
+ *   1. every position after a CR LF (and position 0) is a candidate start
+ *      (hipCUB DeviceSelect); a true request start is always one;
+ *   2. one thread per candidate runs the request state machine from there:
+ *      status, end, key count. Bulk data is skipped by its length, so a
+ *      thread touches O(tokens) bytes, not O(bytes);
+ *   3. next[c] = the candidate at c's end (binary search), or none when c
+ *      failed, is incomplete or ends the stream;
+ *   4. the chain from candidate 0 is marked by pointer jumping
+ *      (ceil(log2 nc) + 1 rounds; round r marks distance [2^(r-1), 2^r));
+ *   5. the marked candidates, compacted in order, are the requests the
+ *      reference parses; then the key count scan, emit, length scan and
+ *      gather of the memcache pipeline (nc_mc_parse.hip).
+ */
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <errno.h>
+#include <stdlib.h>
+
+#include "nc_gpuhash.h"
+
+namespace {
+
+enum : uint8_t { RC_NONE, RC_ARG0, RC_ARG1, RC_ARGN, RC_ARGX, RC_ARGKVX };
+
+struct CmdName {
+    char name[18];
+    uint8_t len;
+    uint8_t cls;
+};
+
+#define A0(s) {s, sizeof(s) - 1, RC_ARG0}
+#define A1(s) {s, sizeof(s) - 1, RC_ARG1}
+#define AN(s) {s, sizeof(s) - 1, RC_ARGN}
+#define AX(s) {s, sizeof(s) - 1, RC_ARGX}
+
+/* lowercase command names of the key classes (redis_arg0/arg1/argn/argx/argkvx,
+ * nc_redis.c:64-334); compared case-insensitively (str*icmp, nc_proto.h:87) */
+__constant__ CmdName kCmds[] = {
+    A0("persist"), A0("pttl"), A0("ttl"), A0("type"), A0("dump"), A0("decr"), A0("get"), A0("getdel"),
+    A0("incr"), A0("strlen"), A0("hgetall"), A0("hkeys"), A0("hlen"), A0("hvals"), A0("llen"), A0("scard"),
+    A0("smembers"), A0("zcard"),
+    A1("expire"), A1("expireat"), A1("pexpire"), A1("pexpireat"), A1("move"), A1("append"), A1("decrby"),
+    A1("getbit"), A1("getset"), A1("incrby"), A1("incrbyfloat"), A1("setnx"), A1("hexists"), A1("hget"),
+    A1("hstrlen"), A1("lindex"), A1("rpoplpush"), A1("sismember"), A1("zrank"), A1("zrevrank"), A1("zscore"),
+    AN("sort"), AN("copy"), AN("bitcount"), AN("bitpos"), AN("bitfield"), AN("exists"), AN("getex"), AN("set"),
+    AN("hdel"), AN("hmget"), AN("hmset"), AN("hscan"), AN("hset"), AN("hrandfield"), AN("lpush"), AN("lpushx"),
+    AN("rpush"), AN("rpushx"), AN("lpop"), AN("rpop"), AN("lpos"), AN("sadd"), AN("sdiff"), AN("sdiffstore"),
+    AN("sinter"), AN("sinterstore"), AN("srem"), AN("sunion"), AN("sunionstore"), AN("srandmember"),
+    AN("sscan"), AN("spop"), AN("smismember"), AN("pfadd"), AN("pfmerge"), AN("pfcount"), AN("zadd"),
+    AN("zdiff"), AN("zdiffstore"), AN("zinter"), AN("zinterstore"), AN("zmscore"), AN("zpopmax"),
+    AN("zpopmin"), AN("zrandmember"), AN("zrange"), AN("zrangebylex"), AN("zrangebyscore"), AN("zrangestore"),
+    AN("zrem"), AN("zrevrange"), AN("zrevrangebylex"), AN("zrevrangebyscore"), AN("zscan"), AN("zunion"),
+    AN("zunionstore"), AN("geodist"), AN("geopos"), AN("geohash"), AN("geoadd"), AN("georadius"),
+    AN("georadiusbymember"), AN("geosearch"), AN("geosearchstore"), AN("restore"),
+    AX("mget"), AX("del"), AX("unlink"), AX("touch"),
+    {"mset", 4, RC_ARGKVX},
+};
+constexpr int kNumCmds = sizeof(kCmds) / sizeof(kCmds[0]);
+
+__device__ uint8_t cmd_class(const uint8_t *__restrict__ m, uint32_t len)
+{
+    if (len < 3 || len > 17) return RC_NONE;
+    for (int e = 0; e < kNumCmds; e++) {
+        if (kCmds[e].len != len) continue;
+        uint32_t i = 0;
+        /* every table byte is a lowercase letter: m | 0x20 matches exactly its two cases */
+        while (i < len && (uint8_t)(m[i] | 0x20u) == (uint8_t)kCmds[e].name[i]) i++;
+        if (i == len) return kCmds[e].cls;
+    }
+    return RC_NONE;
+}
+
+constexpr int32_t kIncomplete = 1; /* the request runs past the stream end */
+
+enum { RS_NARG, RS_NARG_LF, RS_TYPE_LEN, RS_TYPE_LEN_LF, RS_TYPE, RS_TYPE_LF, RS_KEY_LEN, RS_KEY_LEN_LF,
+       RS_KEY, RS_KEY_LF, RS_ARG_LEN, RS_ARG_LEN_LF, RS_ARG, RS_ARG_LF };
+
+/* One request from s[p0]: the state machine of redis_parse_req for the key
+ * classes. Returns the status; on 0, *end is one past its LF and *nkeys its
+ * key count. EMIT also writes each key's span at base + i. */
+template <bool EMIT>
+__device__ int32_t parse_req(const uint8_t *__restrict__ s, uint32_t n, uint32_t p0, uint32_t max_key_len,
+                             uint32_t *end, uint32_t *nkeys, uint32_t *kstart, uint32_t *klen, uint32_t *kreq,
+                             uint32_t base, uint32_t req)
+{
+    if (s[p0] != '*') return NC_GPUHASH_REDIS_EINVAL; /* SW_START (:478-483) */
+    uint32_t narg = 0, rnarg = 0, rlen = 0, kn = 0, token = 0;
+    int state = RS_NARG;
+    uint8_t cls = RC_NONE;
+    bool have_token = false;
+    /* p advances at the bottom: by one byte, or past a bulk string (next_p).
+     * Assigning the for-loop counter inside the switch instead was
+     * miscompiled for gfx950 (the skip was lost; found by the parity tests). */
+    for (uint32_t p = p0 + 1, next_p; p < n; p = next_p) {
+        const uint8_t ch = s[p];
+        next_p = p + 1;
+        switch (state) {
+        case RS_NARG:
+            if (ch >= '0' && ch <= '9') rnarg = rnarg * 10u + (uint32_t)(ch - '0');
+            else if (ch == '\r' && rnarg != 0) { narg = rnarg; state = RS_NARG_LF; }
+            else return NC_GPUHASH_REDIS_EINVAL;
+            break;
+        case RS_NARG_LF:
+        case RS_TYPE_LEN_LF:
+        case RS_KEY_LEN_LF:
+        case RS_ARG_LEN_LF:
+            if (ch != '\n') return NC_GPUHASH_REDIS_EINVAL;
+            state = state == RS_NARG_LF ? RS_TYPE_LEN : state == RS_TYPE_LEN_LF ? RS_TYPE
+                  : state == RS_KEY_LEN_LF ? RS_KEY : RS_ARG;
+            have_token = false;
+            break;
+        case RS_TYPE_LEN:
+        case RS_KEY_LEN:
+        case RS_ARG_LEN:
+            if (!have_token) {
+                if (ch != '$') return NC_GPUHASH_REDIS_EINVAL;
+                have_token = true;
+                token = p;
+                rlen = 0;
+            } else if (ch >= '0' && ch <= '9') {
+                rlen = rlen * 10u + (uint32_t)(ch - '0');
+            } else if (ch == '\r') {
+                if (state == RS_TYPE_LEN && (rlen == 0 || rnarg == 0)) return NC_GPUHASH_REDIS_EINVAL;
+                if (state == RS_KEY_LEN && rlen >= max_key_len) return NC_GPUHASH_REDIS_EKEYLEN;
+                if (state == RS_KEY_LEN && rnarg == 0) return NC_GPUHASH_REDIS_EINVAL;
+                if (state == RS_ARG_LEN && (p - token <= 1 || rnarg == 0)) return NC_GPUHASH_REDIS_EINVAL;
+                rnarg--;
+                state = state == RS_TYPE_LEN ? RS_TYPE_LEN_LF : state == RS_KEY_LEN ? RS_KEY_LEN_LF : RS_ARG_LEN_LF;
+            } else {
+                return NC_GPUHASH_REDIS_EINVAL;
+            }
+            break;
+        case RS_TYPE:
+        case RS_KEY:
+        case RS_ARG: {
+            const uint64_t m = (uint64_t)p + rlen; /* rlen data bytes, then CR */
+            if (m >= n) return kIncomplete;
+            if (s[m] != '\r') return NC_GPUHASH_REDIS_EINVAL;
+            if (state == RS_TYPE) {
+                cls = cmd_class(s + p, rlen);
+                if (cls == RC_NONE) return NC_GPUHASH_REDIS_EUNSUPPORTED;
+                state = RS_TYPE_LF;
+            } else if (state == RS_KEY) {
+                if constexpr (EMIT) {
+                    kstart[base + kn] = p;
+                    klen[base + kn] = rlen;
+                    kreq[base + kn] = req;
+                }
+                kn++;
+                state = RS_KEY_LF;
+            } else {
+                state = RS_ARG_LF;
+            }
+            next_p = (uint32_t)m + 1u;
+            break;
+        }
+        case RS_TYPE_LF:
+            if (ch != '\n' || narg == 1) return NC_GPUHASH_REDIS_EINVAL;
+            state = RS_KEY_LEN;
+            have_token = false;
+            break;
+        case RS_KEY_LF: {
+            if (ch != '\n') return NC_GPUHASH_REDIS_EINVAL;
+            have_token = false;
+            bool fin = false;
+            if (cls == RC_ARG0) {
+                if (rnarg != 0) return NC_GPUHASH_REDIS_EINVAL;
+                fin = true;
+            } else if (cls == RC_ARG1) {
+                if (rnarg != 1) return NC_GPUHASH_REDIS_EINVAL;
+                state = RS_ARG_LEN;
+            } else if (cls == RC_ARGN || cls == RC_ARGX) {
+                if (rnarg == 0) fin = true;
+                else state = cls == RC_ARGX ? RS_KEY_LEN : RS_ARG_LEN;
+            } else { /* argkvx */
+                if (narg % 2 == 0) return NC_GPUHASH_REDIS_EINVAL;
+                state = RS_ARG_LEN;
+            }
+            if (fin) {
+                *end = p + 1;
+                *nkeys = kn;
+                return NC_GPUHASH_REDIS_OK;
+            }
+            break;
+        }
+        case RS_ARG_LF:
+            if (ch != '\n') return NC_GPUHASH_REDIS_EINVAL;
+            have_token = false;
+            if (cls == RC_ARG1) {
+                if (rnarg != 0) return NC_GPUHASH_REDIS_EINVAL;
+                *end = p + 1;
+                *nkeys = kn;
+                return NC_GPUHASH_REDIS_OK;
+            } else if (rnarg == 0) { /* argn, argkvx */
+                *end = p + 1;
+                *nkeys = kn;
+                return NC_GPUHASH_REDIS_OK;
+            }
+            state = cls == RC_ARGN ? RS_ARG_LEN : RS_KEY_LEN;
+            break;
+        }
+    }
+    return kIncomplete;
+}
+
+__global__ void rd_mark_kernel(const uint8_t *__restrict__ s, uint32_t nbytes, uint8_t *__restrict__ flag)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nbytes; i += gridDim.x * 256u)
+        flag[i] = (i == 0 || (i >= 2 && s[i - 1] == '\n' && s[i - 2] == '\r')) ? 1u : 0u;
+}
+
+/* candidate c: parse, then link to the candidate at its end */
+__global__ void rd_cand_kernel(const uint8_t *__restrict__ s, uint32_t n, uint32_t max_key_len,
+                               const uint32_t *__restrict__ cand, uint32_t nc, int8_t *__restrict__ status,
+                               uint32_t *__restrict__ cend, uint32_t *__restrict__ cnk, uint32_t *__restrict__ next,
+                               uint8_t *__restrict__ mark)
+{
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
+    if (c > nc) return;
+    if (c == nc) { /* the sentinel: points at itself */
+        next[nc] = nc;
+        mark[nc] = 0;
+        return;
+    }
+    uint32_t e = 0, k = 0;
+    const int32_t st = parse_req<false>(s, n, cand[c], max_key_len, &e, &k, nullptr, nullptr, nullptr, 0, 0);
+    status[c] = (int8_t)st;
+    cend[c] = e;
+    cnk[c] = k;
+    uint32_t nx = nc;
+    if (st == NC_GPUHASH_REDIS_OK && e < n) {
+        uint32_t lo = c + 1, hi = nc; /* first candidate >= e; e follows a CR LF, so it is one */
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (cand[mid] < e) lo = mid + 1;
+            else hi = mid;
+        }
+        nx = lo;
+    }
+    next[c] = nx;
+    mark[c] = c == 0 ? 1u : 0u;
+}
+
+/* one pointer-jumping round: marked c marks jump[c]; jout = jump o jump */
+__global__ void rd_jump_kernel(const uint32_t *__restrict__ jin, uint32_t *__restrict__ jout, uint8_t *mark,
+                               uint32_t nc)
+{
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
+    if (c > nc) return;
+    const uint32_t j = jin[c];
+    if (c < nc && mark[c]) mark[j] = 1u; /* marks land only on the chain: races only mark early */
+    jout[c] = jin[j];
+}
+
+/* per request r (the r-th marked candidate): key count (ok ones) and status */
+__global__ void rd_req_kernel(const uint32_t *__restrict__ req, uint32_t nreq, const int8_t *__restrict__ cstatus,
+                              const uint32_t *__restrict__ cnk, uint32_t *__restrict__ nk,
+                              int32_t *__restrict__ rstatus)
+{
+    const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+    if (r >= nreq) return;
+    const uint32_t c = req[r];
+    const int32_t st = cstatus[c];
+    nk[r] = st == NC_GPUHASH_REDIS_OK ? cnk[c] : 0u;
+    if (rstatus) rstatus[r] = st;
+}
+
+__global__ void rd_emit_kernel(const uint8_t *__restrict__ s, uint32_t n, uint32_t max_key_len,
+                               const uint32_t *__restrict__ cand, const uint32_t *__restrict__ req, uint32_t nok,
+                               const uint64_t *__restrict__ kbase, uint32_t *__restrict__ kstart,
+                               uint32_t *__restrict__ klen, uint32_t *__restrict__ kreq)
+{
+    const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+    if (r >= nok) return;
+    uint32_t e = 0, k = 0;
+    (void)parse_req<true>(s, n, cand[req[r]], max_key_len, &e, &k, kstart, klen, kreq, (uint32_t)kbase[r], r);
+}
+
+/* one wave per key: lanes copy its bytes (keys run to mbuf_data_size) */
+__global__ void rd_gather_kernel(const uint8_t *__restrict__ s, const uint32_t *__restrict__ kstart,
+                                 const uint64_t *__restrict__ koff, uint32_t nk, uint8_t *__restrict__ keys)
+{
+    const uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (k >= nk) return;
+    const uint64_t src = kstart[k], dst = koff[k], len = koff[k + 1] - koff[k];
+    for (uint64_t j = threadIdx.x & 63u; j < len; j += 64u) keys[dst + j] = s[src + j];
+}
+
+__global__ void rd_pad_kernel(uint8_t *__restrict__ keys, const uint64_t *__restrict__ koff, uint32_t nk)
+{
+    const uint64_t e = koff[nk];
+    if (threadIdx.x < NC_GPUHASH_PAD) keys[e + threadIdx.x] = 0u;
+}
+
+struct Widen {
+    __host__ __device__ uint64_t operator()(uint32_t v) const { return v; }
+};
+
+unsigned grid_of(uint64_t n, unsigned per = 256u)
+{
+    const uint64_t g = (n + per - 1u) / per;
+    return (unsigned)(g == 0 ? 1u : g);
+}
+
+} // namespace
+
+struct nc_gpuhash_redis_parser {
+    uint64_t max_bytes, max_reqs, max_keys, max_cands;
+    uint8_t *flag;    /* candidate flags, per byte */
+    uint32_t *cand;   /* candidate start positions */
+    int8_t *cstatus;  /* per candidate: status of its speculative parse */
+    uint32_t *cend, *cnk;
+    uint32_t *jmp[2]; /* pointer-jumping successor arrays (nc + 1: the sentinel) */
+    uint8_t *mark;    /* on the chain from candidate 0 */
+    uint32_t *req;    /* marked candidates in order = the requests */
+    uint32_t *nk;     /* keys per request */
+    uint64_t *kbase;
+    uint32_t *kstart, *klen, *kreq;
+    uint64_t *misc;   /* [0] selected count */
+    void *tmp;
+    size_t tmp_bytes;
+};
+
+static void rparser_free(nc_gpuhash_redis_parser_t *ps)
+{
+    void *bufs[] = {ps->flag, ps->cand, ps->cstatus, ps->cend, ps->cnk, ps->jmp[0], ps->jmp[1], ps->mark,
+                    ps->req, ps->nk, ps->kbase, ps->kstart, ps->klen, ps->kreq, ps->misc, ps->tmp};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    free(ps);
+}
+
+extern "C" nc_gpuhash_redis_parser_t *nc_gpuhash_redis_parser_create(uint64_t max_bytes, uint64_t max_reqs,
+                                                                     uint64_t max_keys)
+{
+    if (max_bytes == 0 || max_reqs == 0 || max_keys == 0 || max_bytes >= (1ull << 31) || max_reqs >= (1ull << 31) ||
+        max_keys >= (1ull << 31)) {
+        errno = EINVAL;
+        return nullptr;
+    }
+    nc_gpuhash_redis_parser_t *ps = (nc_gpuhash_redis_parser_t *)calloc(1, sizeof(*ps));
+    if (ps == nullptr) {
+        errno = ENOMEM;
+        return nullptr;
+    }
+    ps->max_bytes = max_bytes;
+    ps->max_reqs = max_reqs;
+    ps->max_keys = max_keys;
+    ps->max_cands = max_bytes / 2u + 2u; /* position 0 and one per CR LF */
+    const uint64_t nc1 = ps->max_cands + 1u;
+    size_t t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    hipError_t e = hipcub::DeviceSelect::Flagged(nullptr, t1, hipcub::CountingInputIterator<uint32_t>(0),
+                                                 (uint8_t *)nullptr, (uint32_t *)nullptr, (uint64_t *)nullptr,
+                                                 (int64_t)max_bytes);
+    if (e == hipSuccess)
+        e = hipcub::DeviceSelect::Flagged(nullptr, t4, hipcub::CountingInputIterator<uint32_t>(0),
+                                          (uint8_t *)nullptr, (uint32_t *)nullptr, (uint64_t *)nullptr,
+                                          (int64_t)ps->max_cands);
+    hipcub::TransformInputIterator<uint64_t, Widen, uint32_t *> w0(nullptr, Widen());
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, t2, w0, (uint64_t *)nullptr, (int64_t)max_reqs + 1);
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, t3, w0, (uint64_t *)nullptr, (int64_t)max_keys + 1);
+    size_t t = t1;
+    for (size_t x : {t2, t3, t4}) t = x > t ? x : t;
+    ps->tmp_bytes = t;
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->flag, max_bytes);
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->cand, nc1 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->cstatus, nc1);
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->cend, nc1 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->cnk, nc1 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->jmp[0], nc1 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->jmp[1], nc1 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->mark, nc1);
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->req, nc1 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->nk, (max_reqs + 1) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->kbase, (max_reqs + 1) * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->kstart, max_keys * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->klen, (max_keys + 1) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->kreq, max_keys * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->misc, 8 * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&ps->tmp, ps->tmp_bytes ? ps->tmp_bytes : 16u);
+    if (e != hipSuccess) {
+        rparser_free(ps);
+        errno = e == hipErrorNoDevice ? ENODEV : ENOMEM;
+        return nullptr;
+    }
+    return ps;
+}
+
+extern "C" void nc_gpuhash_redis_parser_destroy(nc_gpuhash_redis_parser_t *ps)
+{
+    if (ps) rparser_free(ps);
+}
+
+extern "C" rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps, const uint8_t *d_stream,
+                                                  uint64_t nbytes, uint32_t max_key_len, uint8_t *d_keys,
+                                                  uint64_t *d_offsets, uint32_t *d_key_req, int32_t *d_req_status,
+                                                  struct nc_gpuhash_redis_result *res, void *stream)
+{
+    if (ps == nullptr || res == nullptr || (nbytes && d_stream == nullptr) || d_offsets == nullptr ||
+        max_key_len == 0) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    if (nbytes > ps->max_bytes) {
+        errno = ENOMEM;
+        return NC_ENOMEM;
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    res->nreqs = res->nkeys = res->consumed = res->first_error = 0;
+    const uint32_t n = (uint32_t)nbytes;
+    hipError_t e = hipSuccess;
+    uint64_t nreq = 0, nk = 0, first_bad = 0, consumed = 0;
+    if (n) {
+        uint64_t nc = 0;
+        hipLaunchKernelGGL(rd_mark_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_stream, n, ps->flag);
+        e = hipGetLastError();
+        if (e == hipSuccess)
+            e = hipcub::DeviceSelect::Flagged(ps->tmp, ps->tmp_bytes, hipcub::CountingInputIterator<uint32_t>(0),
+                                              ps->flag, ps->cand, ps->misc, (int64_t)n, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&nc, ps->misc, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e == hipSuccess) {
+            const uint32_t c32 = (uint32_t)nc;
+            hipLaunchKernelGGL(rd_cand_kernel, dim3(grid_of(nc + 1)), dim3(256), 0, st, d_stream, n, max_key_len,
+                               ps->cand, c32, ps->cstatus, ps->cend, ps->cnk, ps->jmp[0], ps->mark);
+            int cur = 0;
+            for (uint64_t span = 1; span < 2u * (nc + 1); span <<= 1, cur ^= 1)
+                hipLaunchKernelGGL(rd_jump_kernel, dim3(grid_of(nc + 1)), dim3(256), 0, st, ps->jmp[cur],
+                                   ps->jmp[cur ^ 1], ps->mark, c32);
+            e = hipGetLastError();
+            if (e == hipSuccess)
+                e = hipcub::DeviceSelect::Flagged(ps->tmp, ps->tmp_bytes, hipcub::CountingInputIterator<uint32_t>(0),
+                                                  ps->mark, ps->req, ps->misc, (int64_t)nc, st);
+        }
+        uint64_t nm = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(&nm, ps->misc, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        /* the last request on the chain: ok (ends the stream), failed, or incomplete */
+        uint32_t lastc = 0;
+        int8_t lasts = 0;
+        if (e == hipSuccess && nm) e = hipMemcpy(&lastc, ps->req + nm - 1, sizeof(uint32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess && nm) e = hipMemcpy(&lasts, ps->cstatus + lastc, 1, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && nm) {
+            nreq = lasts == kIncomplete ? nm - 1 : nm;
+            first_bad = lasts != NC_GPUHASH_REDIS_OK ? nm - 1 : nm;
+        }
+        if (e == hipSuccess && nreq > ps->max_reqs) {
+            errno = ENOMEM;
+            return NC_ENOMEM;
+        }
+        if (e == hipSuccess && first_bad) {
+            uint32_t lastok = 0, endp = 0;
+            e = hipMemcpy(&lastok, ps->req + first_bad - 1, sizeof(uint32_t), hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(&endp, ps->cend + lastok, sizeof(uint32_t), hipMemcpyDeviceToHost);
+            consumed = endp;
+        }
+        if (e == hipSuccess && nreq) {
+            hipLaunchKernelGGL(rd_req_kernel, dim3(grid_of(nreq)), dim3(256), 0, st, ps->req, (uint32_t)nreq,
+                               ps->cstatus, ps->cnk, ps->nk, d_req_status);
+            e = hipGetLastError();
+            /* nk[first_bad] = 0 so the exclusive scan's last element is the key total */
+            if (e == hipSuccess) e = hipMemsetAsync(ps->nk + first_bad, 0, sizeof(uint32_t), st);
+            hipcub::TransformInputIterator<uint64_t, Widen, uint32_t *> wn(ps->nk, Widen());
+            if (e == hipSuccess)
+                e = hipcub::DeviceScan::ExclusiveSum(ps->tmp, ps->tmp_bytes, wn, ps->kbase, (int64_t)first_bad + 1, st);
+            if (e == hipSuccess) e = hipMemcpyAsync(&nk, ps->kbase + first_bad, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e == hipSuccess && nk > ps->max_keys) {
+                errno = ENOMEM;
+                return NC_ENOMEM;
+            }
+        }
+        if (e == hipSuccess && nk) {
+            uint32_t *kreq = d_key_req ? d_key_req : ps->kreq;
+            hipLaunchKernelGGL(rd_emit_kernel, dim3(grid_of(first_bad)), dim3(256), 0, st, d_stream, n, max_key_len,
+                               ps->cand, ps->req, (uint32_t)first_bad, ps->kbase, ps->kstart, ps->klen, kreq);
+            e = hipGetLastError();
+            if (e == hipSuccess) e = hipMemsetAsync(ps->klen + nk, 0, sizeof(uint32_t), st);
+            hipcub::TransformInputIterator<uint64_t, Widen, uint32_t *> wl(ps->klen, Widen());
+            if (e == hipSuccess)
+                e = hipcub::DeviceScan::ExclusiveSum(ps->tmp, ps->tmp_bytes, wl, d_offsets, (int64_t)nk + 1, st);
+            if (e == hipSuccess && d_keys) {
+                hipLaunchKernelGGL(rd_gather_kernel, dim3(grid_of(nk, 4u)), dim3(256), 0, st, d_stream, ps->kstart,
+                                   d_offsets, (uint32_t)nk, d_keys);
+                hipLaunchKernelGGL(rd_pad_kernel, dim3(1), dim3(64), 0, st, d_keys, d_offsets, (uint32_t)nk);
+                e = hipGetLastError();
+            }
+        }
+    }
+    if (e == hipSuccess && nk == 0) e = hipMemsetAsync(d_offsets, 0, sizeof(uint64_t), st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        errno = e == hipErrorNoDevice ? ENODEV : EIO;
+        return NC_ERROR;
+    }
+    res->nreqs = nreq;
+    res->nkeys = nk;
+    res->first_error = first_bad;
+    res->consumed = consumed;
+    return NC_OK;
+}

@@ -272,6 +272,47 @@ class McParser:
         return keys, off[: nk + 1], kreq[:nk], status[:nr], info
 
 
+class RedisParser(McParser):
+    """Key extraction on the device from pipelined redis (RESP) requests of the
+    arg0/arg1/argn/argx/argkvx classes (nc_gpuhash_redis_parse_device;
+    redis_parse_req, src/proto/nc_redis.c:460-1900)."""
+
+    def __init__(self, max_bytes: int, max_reqs: int, max_keys: int, max_key_len: int = 16336):
+        self._lib = L.lib()
+        self._h = self._lib.nc_gpuhash_redis_parser_create(max_bytes, max_reqs, max_keys)
+        if not self._h:
+            raise L.NcError(ctypes.get_errno(), "nc_gpuhash_redis_parser_create failed")
+        self.max_keys, self.max_reqs, self.max_bytes = max_keys, max_reqs, max_bytes
+        self.max_key_len = max_key_len  # mbuf_data_size(): 16 KiB mbuf less its header (src/nc_mbuf.c)
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.nc_gpuhash_redis_parser_destroy(self._h)
+            self._h = None
+
+    def parse(self, stream, stream_handle=None):
+        """As McParser.parse, with NC_GPUHASH_REDIS_* statuses."""
+        import torch
+
+        dev = stream.device
+        nbytes = stream.numel()
+        keys = torch.empty(nbytes + L.NC_GPUHASH_PAD, dtype=torch.uint8, device=dev)
+        off = torch.empty(self.max_keys + 1, dtype=torch.int64, device=dev)
+        kreq = torch.empty(self.max_keys, dtype=torch.int32, device=dev)
+        status = torch.empty(self.max_reqs, dtype=torch.int32, device=dev)
+        res = L.NcRedisResult()
+        L.check(
+            self._lib.nc_gpuhash_redis_parse_device(
+                self._h, stream.data_ptr(), nbytes, self.max_key_len, keys.data_ptr(), off.data_ptr(),
+                kreq.data_ptr(), status.data_ptr(), ctypes.byref(res), _stream_handle(stream_handle),
+            ),
+            "nc_gpuhash_redis_parse_device",
+        )
+        nk, nr = int(res.nkeys), int(res.nreqs)
+        info = {"nreqs": nr, "nkeys": nk, "first_error": int(res.first_error), "consumed": int(res.consumed)}
+        return keys, off[: nk + 1], kreq[:nk], status[:nr], info
+
+
 def time_batch_device(hash_: int | str, keys, offsets, out, iters: int, stream=None, shape=None) -> float:
     """Mean ms per launch over `iters` launches, timed by hipEvents on the launch stream."""
     mode = mode_of(hash_)
