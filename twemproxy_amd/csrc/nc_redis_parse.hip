@@ -18,8 +18,11 @@
  *
  * RESP requests are length-prefixed and binary-safe, so request boundaries are
  * not visible in the bytes. The device parses speculatively:
- *   1. every position after a CR LF (and position 0) is a candidate start
- *      (hipCUB DeviceSelect); a true request start is always one;
+ *   1. every '*' after a CR LF (and position 0) is a candidate start
+ *      (hipCUB DeviceSelect); a true request start is always one, except a
+ *      start that is not '*': that request fails at its first byte
+ *      (SW_START, :478-483), so an ok chain that stops short of the stream
+ *      end is followed by one failing request;
  *   2. one thread per candidate runs the request state machine from there:
  *      status, end, key count. Bulk data is skipped by its length, so a
  *      thread touches O(tokens) bytes, not O(bytes);
@@ -227,7 +230,7 @@ __device__ int32_t parse_req(const uint8_t *__restrict__ s, uint32_t n, uint32_t
 __global__ void rd_mark_kernel(const uint8_t *__restrict__ s, uint32_t nbytes, uint8_t *__restrict__ flag)
 {
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nbytes; i += gridDim.x * 256u)
-        flag[i] = (i == 0 || (i >= 2 && s[i - 1] == '\n' && s[i - 2] == '\r')) ? 1u : 0u;
+        flag[i] = (i == 0 || (s[i] == '*' && i >= 2 && s[i - 1] == '\n' && s[i - 2] == '\r')) ? 1u : 0u;
 }
 
 /* candidate c: parse, then link to the candidate at its end */
@@ -249,8 +252,8 @@ __global__ void rd_cand_kernel(const uint8_t *__restrict__ s, uint32_t n, uint32
     cend[c] = e;
     cnk[c] = k;
     uint32_t nx = nc;
-    if (st == NC_GPUHASH_REDIS_OK && e < n) {
-        uint32_t lo = c + 1, hi = nc; /* first candidate >= e; e follows a CR LF, so it is one */
+    if (st == NC_GPUHASH_REDIS_OK && e < n && s[e] == '*') {
+        uint32_t lo = c + 1, hi = nc; /* first candidate >= e; e follows a CR LF and holds '*': it is one */
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
             if (cand[mid] < e) lo = mid + 1;
@@ -271,6 +274,23 @@ __global__ void rd_jump_kernel(const uint32_t *__restrict__ jin, uint32_t *__res
     const uint32_t j = jin[c];
     if (c < nc && mark[c]) mark[j] = 1u; /* marks land only on the chain: races only mark early */
     jout[c] = jin[j];
+}
+
+/* the chain's last request: [1] its candidate, [2] its status, [3] its end */
+__global__ void rd_tail_kernel(const uint32_t *__restrict__ req, const int8_t *__restrict__ cstatus,
+                               const uint32_t *__restrict__ cend, uint64_t *misc)
+{
+    const uint64_t nm = misc[0];
+    const uint32_t c = nm ? req[nm - 1] : 0u;
+    misc[1] = c;
+    misc[2] = (uint64_t)(int64_t)cstatus[c];
+    misc[3] = cend[c];
+}
+
+/* the request after an ok chain whose next byte is not '*': SW_START fails (:478-483) */
+__global__ void rd_bad_start_kernel(int32_t *__restrict__ rstatus, uint64_t r)
+{
+    rstatus[r] = NC_GPUHASH_REDIS_EINVAL;
 }
 
 /* per request r (the r-th marked candidate): key count (ok ones) and status */
@@ -453,16 +473,19 @@ extern "C" rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps
                 e = hipcub::DeviceSelect::Flagged(ps->tmp, ps->tmp_bytes, hipcub::CountingInputIterator<uint32_t>(0),
                                                   ps->mark, ps->req, ps->misc, (int64_t)nc, st);
         }
-        uint64_t nm = 0;
-        if (e == hipSuccess) e = hipMemcpyAsync(&nm, ps->misc, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+        uint64_t tail[4] = {0, 0, 0, 0}; /* marked count, last candidate, its status, its end */
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(rd_tail_kernel, dim3(1), dim3(1), 0, st, ps->req, ps->cstatus, ps->cend, ps->misc);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(tail, ps->misc, sizeof(tail), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
-        /* the last request on the chain: ok (ends the stream), failed, or incomplete */
-        uint32_t lastc = 0;
-        int8_t lasts = 0;
-        if (e == hipSuccess && nm) e = hipMemcpy(&lastc, ps->req + nm - 1, sizeof(uint32_t), hipMemcpyDeviceToHost);
-        if (e == hipSuccess && nm) e = hipMemcpy(&lasts, ps->cstatus + lastc, 1, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && nm) {
-            nreq = lasts == kIncomplete ? nm - 1 : nm;
+        const uint64_t nm = tail[0];
+        const int64_t lasts = (int64_t)tail[2];
+        /* an ok chain that stops before the stream end: the next byte is not '*', a failing request */
+        const bool bad_start = nm && lasts == NC_GPUHASH_REDIS_OK && tail[3] < n;
+        if (nm) {
+            nreq = lasts == kIncomplete ? nm - 1 : nm + (bad_start ? 1u : 0u);
             first_bad = lasts != NC_GPUHASH_REDIS_OK ? nm - 1 : nm;
         }
         if (e == hipSuccess && nreq > ps->max_reqs) {
@@ -470,14 +493,18 @@ extern "C" rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps
             return NC_ENOMEM;
         }
         if (e == hipSuccess && first_bad) {
-            uint32_t lastok = 0, endp = 0;
-            e = hipMemcpy(&lastok, ps->req + first_bad - 1, sizeof(uint32_t), hipMemcpyDeviceToHost);
-            if (e == hipSuccess) e = hipMemcpy(&endp, ps->cend + lastok, sizeof(uint32_t), hipMemcpyDeviceToHost);
+            uint32_t lastok = (uint32_t)tail[1], endp = (uint32_t)tail[3];
+            if (first_bad != nm) { /* the last marked one failed: the ok one before it */
+                e = hipMemcpy(&lastok, ps->req + first_bad - 1, sizeof(uint32_t), hipMemcpyDeviceToHost);
+                if (e == hipSuccess) e = hipMemcpy(&endp, ps->cend + lastok, sizeof(uint32_t), hipMemcpyDeviceToHost);
+            }
             consumed = endp;
         }
         if (e == hipSuccess && nreq) {
-            hipLaunchKernelGGL(rd_req_kernel, dim3(grid_of(nreq)), dim3(256), 0, st, ps->req, (uint32_t)nreq,
+            hipLaunchKernelGGL(rd_req_kernel, dim3(grid_of(nm)), dim3(256), 0, st, ps->req, (uint32_t)(nreq < nm ? nreq : nm),
                                ps->cstatus, ps->cnk, ps->nk, d_req_status);
+            if (bad_start && d_req_status)
+                hipLaunchKernelGGL(rd_bad_start_kernel, dim3(1), dim3(1), 0, st, d_req_status, nm);
             e = hipGetLastError();
             /* nk[first_bad] = 0 so the exclusive scan's last element is the key total */
             if (e == hipSuccess) e = hipMemsetAsync(ps->nk + first_bad, 0, sizeof(uint32_t), st);
