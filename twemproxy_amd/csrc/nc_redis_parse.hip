@@ -19,7 +19,7 @@
  * RESP requests are length-prefixed and binary-safe, so request boundaries are
  * not visible in the bytes. The device parses speculatively:
  *   1. every '*' after a CR LF (and position 0) is a candidate start
- *      (hipCUB DeviceSelect); a true request start is always one, except a
+ *      (a two-pass count / scan / write select over 16-B blocks); a true request start is always one, except a
  *      start that is not '*': that request fails at its first byte
  *      (SW_START, :478-483), so an ok chain that stops short of the stream
  *      end is followed by one failing request;
@@ -227,10 +227,57 @@ __device__ int32_t parse_req(const uint8_t *__restrict__ s, uint32_t n, uint32_t
     return kIncomplete;
 }
 
-__global__ void rd_mark_kernel(const uint8_t *__restrict__ s, uint32_t nbytes, uint8_t *__restrict__ flag)
+/* Candidate starts (position 0, or '*' right after CR LF) of the 16-B aligned
+ * block `blk` of the stream as a bit mask; the stream starts `delta` bytes
+ * into block 0. One 16-B load per block plus the 4 bytes before it: aligned
+ * loads that hold a stream byte stay inside the stream's pages. */
+__device__ __forceinline__ uint32_t cand_mask(const uint8_t *__restrict__ sa, uint32_t delta, uint32_t n, uint32_t blk)
 {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nbytes; i += gridDim.x * 256u)
-        flag[i] = (i == 0 || (s[i] == '*' && i >= 2 && s[i - 1] == '\n' && s[i - 2] == '\r')) ? 1u : 0u;
+    const uint4 v = *reinterpret_cast<const uint4 *>(sa + (uint64_t)blk * 16u);
+    const uint32_t prev = blk ? *reinterpret_cast<const uint32_t *>(sa + (uint64_t)blk * 16u - 4u) : 0u;
+    const uint32_t w[5] = {prev, v.x, v.y, v.z, v.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int j = k + 4;
+        const uint32_t c0 = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+        const uint32_t c1 = (w[(j - 1) >> 2] >> (8 * ((j - 1) & 3))) & 0xffu;
+        const uint32_t c2 = (w[(j - 2) >> 2] >> (8 * ((j - 2) & 3))) & 0xffu;
+        const int64_t i = (int64_t)blk * 16 + k - delta;
+        const bool hit = i == 0 || (i >= 2 && i < (int64_t)n && c0 == '*' && c1 == '\n' && c2 == '\r');
+        m |= hit ? (1u << k) : 0u;
+    }
+    return m;
+}
+
+/* pass 1: candidates per workgroup of 256 blocks (4 KiB of stream) */
+__global__ void rd_cand_count_kernel(const uint8_t *__restrict__ sa, uint32_t delta, uint32_t n, uint32_t nblk,
+                                     uint32_t *__restrict__ wg_count)
+{
+    using Reduce = hipcub::BlockReduce<uint32_t, 256>;
+    __shared__ typename Reduce::TempStorage tmp;
+    const uint32_t blk = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t c = blk < nblk ? (uint32_t)__popc(cand_mask(sa, delta, n, blk)) : 0u;
+    const uint32_t tot = Reduce(tmp).Sum(c);
+    if (threadIdx.x == 0) wg_count[blockIdx.x] = tot;
+}
+
+/* pass 2: after the exclusive scan of wg_count, write positions in order */
+__global__ void rd_cand_write_kernel(const uint8_t *__restrict__ sa, uint32_t delta, uint32_t n, uint32_t nblk,
+                                     const uint32_t *__restrict__ wg_base, uint32_t *__restrict__ cand)
+{
+    using Scan = hipcub::BlockScan<uint32_t, 256>;
+    __shared__ typename Scan::TempStorage tmp;
+    const uint32_t blk = blockIdx.x * 256u + threadIdx.x;
+    uint32_t m = blk < nblk ? cand_mask(sa, delta, n, blk) : 0u;
+    uint32_t at = 0;
+    Scan(tmp).ExclusiveSum((uint32_t)__popc(m), at);
+    at += wg_base[blockIdx.x];
+    while (m) {
+        const int k = __ffs(m) - 1;
+        m &= m - 1u;
+        cand[at++] = (uint32_t)((int64_t)blk * 16 + k - delta);
+    }
 }
 
 /* candidate c: parse, then link to the candidate at its end */
@@ -317,14 +364,14 @@ __global__ void rd_emit_kernel(const uint8_t *__restrict__ s, uint32_t n, uint32
     (void)parse_req<true>(s, n, cand[req[r]], max_key_len, &e, &k, kstart, klen, kreq, (uint32_t)kbase[r], r);
 }
 
-/* one wave per key: lanes copy its bytes (keys run to mbuf_data_size) */
+/* 8 lanes per key copy its bytes (C2-like keys are ~19 B; longer ones loop) */
 __global__ void rd_gather_kernel(const uint8_t *__restrict__ s, const uint32_t *__restrict__ kstart,
                                  const uint64_t *__restrict__ koff, uint32_t nk, uint8_t *__restrict__ keys)
 {
-    const uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t k = blockIdx.x * 32u + (threadIdx.x >> 3);
     if (k >= nk) return;
     const uint64_t src = kstart[k], dst = koff[k], len = koff[k + 1] - koff[k];
-    for (uint64_t j = threadIdx.x & 63u; j < len; j += 64u) keys[dst + j] = s[src + j];
+    for (uint64_t j = threadIdx.x & 7u; j < len; j += 8u) keys[dst + j] = s[src + j];
 }
 
 __global__ void rd_pad_kernel(uint8_t *__restrict__ keys, const uint64_t *__restrict__ koff, uint32_t nk)
@@ -347,7 +394,8 @@ unsigned grid_of(uint64_t n, unsigned per = 256u)
 
 struct nc_gpuhash_redis_parser {
     uint64_t max_bytes, max_reqs, max_keys, max_cands;
-    uint8_t *flag;    /* candidate flags, per byte */
+    uint32_t *wgc, *wgb; /* candidates per workgroup of the select, and their exclusive scan */
+    uint64_t max_wg;
     uint32_t *cand;   /* candidate start positions */
     int8_t *cstatus;  /* per candidate: status of its speculative parse */
     uint32_t *cend, *cnk;
@@ -364,7 +412,7 @@ struct nc_gpuhash_redis_parser {
 
 static void rparser_free(nc_gpuhash_redis_parser_t *ps)
 {
-    void *bufs[] = {ps->flag, ps->cand, ps->cstatus, ps->cend, ps->cnk, ps->jmp[0], ps->jmp[1], ps->mark,
+    void *bufs[] = {ps->wgc, ps->wgb, ps->cand, ps->cstatus, ps->cend, ps->cnk, ps->jmp[0], ps->jmp[1], ps->mark,
                     ps->req, ps->nk, ps->kbase, ps->kstart, ps->klen, ps->kreq, ps->misc, ps->tmp};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -390,9 +438,9 @@ extern "C" nc_gpuhash_redis_parser_t *nc_gpuhash_redis_parser_create(uint64_t ma
     ps->max_cands = max_bytes / 2u + 2u; /* position 0 and one per CR LF */
     const uint64_t nc1 = ps->max_cands + 1u;
     size_t t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-    hipError_t e = hipcub::DeviceSelect::Flagged(nullptr, t1, hipcub::CountingInputIterator<uint32_t>(0),
-                                                 (uint8_t *)nullptr, (uint32_t *)nullptr, (uint64_t *)nullptr,
-                                                 (int64_t)max_bytes);
+    ps->max_wg = (max_bytes + 15u) / 16u / 256u + 2u;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                    (int64_t)ps->max_wg + 1);
     if (e == hipSuccess)
         e = hipcub::DeviceSelect::Flagged(nullptr, t4, hipcub::CountingInputIterator<uint32_t>(0),
                                           (uint8_t *)nullptr, (uint32_t *)nullptr, (uint64_t *)nullptr,
@@ -403,7 +451,8 @@ extern "C" nc_gpuhash_redis_parser_t *nc_gpuhash_redis_parser_create(uint64_t ma
     size_t t = t1;
     for (size_t x : {t2, t3, t4}) t = x > t ? x : t;
     ps->tmp_bytes = t;
-    if (e == hipSuccess) e = hipMalloc((void **)&ps->flag, max_bytes);
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->wgc, (ps->max_wg + 1) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->wgb, (ps->max_wg + 1) * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void **)&ps->cand, nc1 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void **)&ps->cstatus, nc1);
     if (e == hipSuccess) e = hipMalloc((void **)&ps->cend, nc1 * sizeof(uint32_t));
@@ -453,13 +502,23 @@ extern "C" rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps
     uint64_t nreq = 0, nk = 0, first_bad = 0, consumed = 0;
     if (n) {
         uint64_t nc = 0;
-        hipLaunchKernelGGL(rd_mark_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_stream, n, ps->flag);
+        const uint32_t delta = (uint32_t)(reinterpret_cast<uintptr_t>(d_stream) & 15u);
+        const uint8_t *sa = d_stream - delta;
+        const uint32_t nblk = (uint32_t)((n + delta + 15u) / 16u), nwg = (nblk + 255u) / 256u;
+        hipLaunchKernelGGL(rd_cand_count_kernel, dim3(nwg), dim3(256), 0, st, sa, delta, n, nblk, ps->wgc);
         e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemsetAsync(ps->wgc + nwg, 0, sizeof(uint32_t), st);
         if (e == hipSuccess)
-            e = hipcub::DeviceSelect::Flagged(ps->tmp, ps->tmp_bytes, hipcub::CountingInputIterator<uint32_t>(0),
-                                              ps->flag, ps->cand, ps->misc, (int64_t)n, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(&nc, ps->misc, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+            e = hipcub::DeviceScan::ExclusiveSum(ps->tmp, ps->tmp_bytes, ps->wgc, ps->wgb, (int64_t)nwg + 1, st);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(rd_cand_write_kernel, dim3(nwg), dim3(256), 0, st, sa, delta, n, nblk,
+                               ps->wgb, ps->cand);
+            e = hipGetLastError();
+        }
+        uint32_t nc32 = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(&nc32, ps->wgb + nwg, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
+        nc = nc32;
         if (e == hipSuccess) {
             const uint32_t c32 = (uint32_t)nc;
             hipLaunchKernelGGL(rd_cand_kernel, dim3(grid_of(nc + 1)), dim3(256), 0, st, d_stream, n, max_key_len,
@@ -528,7 +587,7 @@ extern "C" rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps
             if (e == hipSuccess)
                 e = hipcub::DeviceScan::ExclusiveSum(ps->tmp, ps->tmp_bytes, wl, d_offsets, (int64_t)nk + 1, st);
             if (e == hipSuccess && d_keys) {
-                hipLaunchKernelGGL(rd_gather_kernel, dim3(grid_of(nk, 4u)), dim3(256), 0, st, d_stream, ps->kstart,
+                hipLaunchKernelGGL(rd_gather_kernel, dim3(grid_of(nk, 32u)), dim3(256), 0, st, d_stream, ps->kstart,
                                    d_offsets, (uint32_t)nk, d_keys);
                 hipLaunchKernelGGL(rd_pad_kernel, dim3(1), dim3(64), 0, st, d_keys, d_offsets, (uint32_t)nk);
                 e = hipGetLastError();
