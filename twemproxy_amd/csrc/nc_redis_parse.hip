@@ -28,8 +28,8 @@
  *      thread touches O(tokens) bytes, not O(bytes);
  *   3. next[c] = the candidate at c's end (binary search), or none when c
  *      failed, is incomplete or ends the stream;
- *   4. the chain from candidate 0 is marked by pointer jumping
- *      (ceil(log2 nc) + 1 rounds; round r marks distance [2^(r-1), 2^r));
+ *   4. the chain from candidate 0 is marked by radix-4 pointer jumping
+ *      (about log4(2 nc) rounds; after round r distances [0, 4^r) are marked);
  *   5. the marked candidates, compacted in order, are the requests the
  *      reference parses; then the key count scan, emit, length scan and
  *      gather of the memcache pipeline (nc_mc_parse.hip).
@@ -312,15 +312,20 @@ __global__ void rd_cand_kernel(const uint8_t *__restrict__ s, uint32_t n, uint32
     mark[c] = c == 0 ? 1u : 0u;
 }
 
-/* one pointer-jumping round: marked c marks jump[c]; jout = jump o jump */
+/* one pointer-jumping round of radix 4: with jin = next^d, a marked c marks
+ * c + d, c + 2d, c + 3d along the chain; jout = next^(4d) */
 __global__ void rd_jump_kernel(const uint32_t *__restrict__ jin, uint32_t *__restrict__ jout, uint8_t *mark,
                                uint32_t nc)
 {
     const uint32_t c = blockIdx.x * 256u + threadIdx.x;
     if (c > nc) return;
-    const uint32_t j = jin[c];
-    if (c < nc && mark[c]) mark[j] = 1u; /* marks land only on the chain: races only mark early */
-    jout[c] = jin[j];
+    const uint32_t j1 = jin[c], j2 = jin[j1], j3 = jin[j2];
+    if (c < nc && mark[c]) { /* marks land only on the chain: races only mark early */
+        mark[j1] = 1u;
+        mark[j2] = 1u;
+        mark[j3] = 1u;
+    }
+    jout[c] = jin[j3];
 }
 
 /* the chain's last request: [1] its candidate, [2] its status, [3] its end */
@@ -524,7 +529,7 @@ extern "C" rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps
             hipLaunchKernelGGL(rd_cand_kernel, dim3(grid_of(nc + 1)), dim3(256), 0, st, d_stream, n, max_key_len,
                                ps->cand, c32, ps->cstatus, ps->cend, ps->cnk, ps->jmp[0], ps->mark);
             int cur = 0;
-            for (uint64_t span = 1; span < 2u * (nc + 1); span <<= 1, cur ^= 1)
+            for (uint64_t span = 1; span < 2u * (nc + 1); span <<= 2, cur ^= 1)
                 hipLaunchKernelGGL(rd_jump_kernel, dim3(grid_of(nc + 1)), dim3(256), 0, st, ps->jmp[cur],
                                    ps->jmp[cur ^ 1], ps->mark, c32);
             e = hipGetLastError();
