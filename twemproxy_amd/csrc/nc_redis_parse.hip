@@ -101,7 +101,8 @@ enum { RS_NARG, RS_NARG_LF, RS_TYPE_LEN, RS_TYPE_LEN_LF, RS_TYPE, RS_TYPE_LF, RS
 
 /* One request from s[p0]: the state machine of redis_parse_req for the key
  * classes. Returns the status; on 0, *end is one past its LF and *nkeys its
- * key count. EMIT also writes each key's span at base + i. */
+ * key count. EMIT writes each key's span at base + i; the count pass writes
+ * the first key's span to *kstart, *klen. */
 template <bool EMIT>
 __device__ int32_t parse_req(const uint8_t *__restrict__ s, uint32_t n, uint32_t p0, uint32_t max_key_len,
                              uint32_t *end, uint32_t *nkeys, uint32_t *kstart, uint32_t *klen, uint32_t *kreq,
@@ -169,6 +170,9 @@ __device__ int32_t parse_req(const uint8_t *__restrict__ s, uint32_t n, uint32_t
                     kstart[base + kn] = p;
                     klen[base + kn] = rlen;
                     kreq[base + kn] = req;
+                } else if (kn == 0) { /* count pass: the first key's span in *kstart, *klen */
+                    *kstart = p;
+                    *klen = rlen;
                 }
                 kn++;
                 state = RS_KEY_LF;
@@ -283,8 +287,8 @@ __global__ void rd_cand_write_kernel(const uint8_t *__restrict__ sa, uint32_t de
 /* candidate c: parse, then link to the candidate at its end */
 __global__ void rd_cand_kernel(const uint8_t *__restrict__ s, uint32_t n, uint32_t max_key_len,
                                const uint32_t *__restrict__ cand, uint32_t nc, int8_t *__restrict__ status,
-                               uint32_t *__restrict__ cend, uint32_t *__restrict__ cnk, uint32_t *__restrict__ next,
-                               uint8_t *__restrict__ mark)
+                               uint32_t *__restrict__ cend, uint32_t *__restrict__ cnk, uint32_t *__restrict__ ck0s,
+                               uint32_t *__restrict__ ck0l, uint32_t *__restrict__ next, uint8_t *__restrict__ mark)
 {
     const uint32_t c = blockIdx.x * 256u + threadIdx.x;
     if (c > nc) return;
@@ -293,11 +297,13 @@ __global__ void rd_cand_kernel(const uint8_t *__restrict__ s, uint32_t n, uint32
         mark[nc] = 0;
         return;
     }
-    uint32_t e = 0, k = 0;
-    const int32_t st = parse_req<false>(s, n, cand[c], max_key_len, &e, &k, nullptr, nullptr, nullptr, 0, 0);
+    uint32_t e = 0, k = 0, k0s = 0, k0l = 0;
+    const int32_t st = parse_req<false>(s, n, cand[c], max_key_len, &e, &k, &k0s, &k0l, nullptr, 0, 0);
     status[c] = (int8_t)st;
     cend[c] = e;
     cnk[c] = k;
+    ck0s[c] = k0s;
+    ck0l[c] = k0l;
     uint32_t nx = nc;
     if (st == NC_GPUHASH_REDIS_OK && e < n && s[e] == '*') {
         uint32_t lo = c + 1, hi = nc; /* first candidate >= e; e follows a CR LF and holds '*': it is one */
@@ -360,13 +366,21 @@ __global__ void rd_req_kernel(const uint32_t *__restrict__ req, uint32_t nreq, c
 
 __global__ void rd_emit_kernel(const uint8_t *__restrict__ s, uint32_t n, uint32_t max_key_len,
                                const uint32_t *__restrict__ cand, const uint32_t *__restrict__ req, uint32_t nok,
-                               const uint64_t *__restrict__ kbase, uint32_t *__restrict__ kstart,
-                               uint32_t *__restrict__ klen, uint32_t *__restrict__ kreq)
+                               const uint32_t *__restrict__ cnk, const uint32_t *__restrict__ ck0s,
+                               const uint32_t *__restrict__ ck0l, const uint64_t *__restrict__ kbase,
+                               uint32_t *__restrict__ kstart, uint32_t *__restrict__ klen, uint32_t *__restrict__ kreq)
 {
     const uint32_t r = blockIdx.x * 256u + threadIdx.x;
     if (r >= nok) return;
-    uint32_t e = 0, k = 0;
-    (void)parse_req<true>(s, n, cand[req[r]], max_key_len, &e, &k, kstart, klen, kreq, (uint32_t)kbase[r], r);
+    const uint32_t c = req[r], nkc = cnk[c], b = (uint32_t)kbase[r];
+    if (nkc == 1) { /* one key (get, set, ...): its span is known from the count pass */
+        kstart[b] = ck0s[c];
+        klen[b] = ck0l[c];
+        kreq[b] = r;
+    } else if (nkc > 1) { /* mget, del, mset, ...: parse again */
+        uint32_t e = 0, k = 0;
+        (void)parse_req<true>(s, n, cand[c], max_key_len, &e, &k, kstart, klen, kreq, b, r);
+    }
 }
 
 /* 8 lanes per key copy its bytes (C2-like keys are ~19 B; longer ones loop) */
@@ -404,6 +418,7 @@ struct nc_gpuhash_redis_parser {
     uint32_t *cand;   /* candidate start positions */
     int8_t *cstatus;  /* per candidate: status of its speculative parse */
     uint32_t *cend, *cnk;
+    uint32_t *ck0s, *ck0l; /* per candidate: the first key's span */
     uint32_t *jmp[2]; /* pointer-jumping successor arrays (nc + 1: the sentinel) */
     uint8_t *mark;    /* on the chain from candidate 0 */
     uint32_t *req;    /* marked candidates in order = the requests */
@@ -417,7 +432,7 @@ struct nc_gpuhash_redis_parser {
 
 static void rparser_free(nc_gpuhash_redis_parser_t *ps)
 {
-    void *bufs[] = {ps->wgc, ps->wgb, ps->cand, ps->cstatus, ps->cend, ps->cnk, ps->jmp[0], ps->jmp[1], ps->mark,
+    void *bufs[] = {ps->wgc, ps->wgb, ps->cand, ps->cstatus, ps->cend, ps->cnk, ps->ck0s, ps->ck0l, ps->jmp[0], ps->jmp[1], ps->mark,
                     ps->req, ps->nk, ps->kbase, ps->kstart, ps->klen, ps->kreq, ps->misc, ps->tmp};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -462,6 +477,8 @@ extern "C" nc_gpuhash_redis_parser_t *nc_gpuhash_redis_parser_create(uint64_t ma
     if (e == hipSuccess) e = hipMalloc((void **)&ps->cstatus, nc1);
     if (e == hipSuccess) e = hipMalloc((void **)&ps->cend, nc1 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void **)&ps->cnk, nc1 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->ck0s, nc1 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->ck0l, nc1 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void **)&ps->jmp[0], nc1 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void **)&ps->jmp[1], nc1 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void **)&ps->mark, nc1);
@@ -527,7 +544,8 @@ extern "C" rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps
         if (e == hipSuccess) {
             const uint32_t c32 = (uint32_t)nc;
             hipLaunchKernelGGL(rd_cand_kernel, dim3(grid_of(nc + 1)), dim3(256), 0, st, d_stream, n, max_key_len,
-                               ps->cand, c32, ps->cstatus, ps->cend, ps->cnk, ps->jmp[0], ps->mark);
+                               ps->cand, c32, ps->cstatus, ps->cend, ps->cnk, ps->ck0s, ps->ck0l, ps->jmp[0],
+                               ps->mark);
             int cur = 0;
             for (uint64_t span = 1; span < 2u * (nc + 1); span <<= 2, cur ^= 1)
                 hipLaunchKernelGGL(rd_jump_kernel, dim3(grid_of(nc + 1)), dim3(256), 0, st, ps->jmp[cur],
@@ -585,7 +603,8 @@ extern "C" rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps
         if (e == hipSuccess && nk) {
             uint32_t *kreq = d_key_req ? d_key_req : ps->kreq;
             hipLaunchKernelGGL(rd_emit_kernel, dim3(grid_of(first_bad)), dim3(256), 0, st, d_stream, n, max_key_len,
-                               ps->cand, ps->req, (uint32_t)first_bad, ps->kbase, ps->kstart, ps->klen, kreq);
+                               ps->cand, ps->req, (uint32_t)first_bad, ps->cnk, ps->ck0s, ps->ck0l, ps->kbase,
+                               ps->kstart, ps->klen, kreq);
             e = hipGetLastError();
             if (e == hipSuccess) e = hipMemsetAsync(ps->klen + nk, 0, sizeof(uint32_t), st);
             hipcub::TransformInputIterator<uint64_t, Widen, uint32_t *> wl(ps->klen, Widen());
