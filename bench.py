@@ -302,6 +302,14 @@ def main():
         read_ceiling(t, res["c3_fnv1a_64"]["roofline"], keys3)
         del keys3, off3, out3
 
+    # ---- redis key extraction, rank 0: 2^20 pipelined RESP GETs over
+    # the first C2 keys (binary-safe), parsed on the device into the CSR above
+    if rank == 0 and not args.no_extra:
+        try:
+            res["redis_key_extraction"] = redis_leg(t, torch, np, spec, dev)
+        except Exception as e:  # reported beside the headline, never instead of it
+            res["redis_key_extraction"] = {"error": repr(e)}
+
     # ---- CPU baseline (rank 0, N = 1)
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
@@ -315,6 +323,37 @@ def main():
 
         dist.barrier()
         dist.destroy_process_group()
+
+
+def redis_leg(t, torch, np, spec, dev, nreq=1 << 20, reps=10):
+    """nc_gpuhash_redis_parse_device over nreq "*2 $3 get $<len> <key>" requests
+    (wall time per parse, host syncs included: the counts size the launches)."""
+    import time
+
+    kh, oh = t.synth_host(spec, 0, nreq)
+    kb = kh.tobytes()
+    stream = b"".join(b"*2\r\n$3\r\nget\r\n$%d\r\n%s\r\n" % (int(oh[i + 1] - oh[i]), kb[int(oh[i]): int(oh[i + 1])])
+                      for i in range(nreq))
+    sd = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).to(dev)
+    with t.RedisParser(max_bytes=len(stream) + 16, max_reqs=nreq + 1, max_keys=nreq + 1) as ps:
+        for _ in range(2):
+            ps.parse(sd)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            keys, off, _, _, info = ps.parse(sd)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        if info["nkeys"] != nreq or info["consumed"] != len(stream):
+            raise AssertionError(f"redis parse: {info}")
+        o = off.cpu().numpy()
+        if not np.array_equal(o, oh.astype(np.int64)):
+            raise AssertionError("redis parse: key offsets differ from the generator's")
+        if not np.array_equal(keys[: int(oh[-1])].cpu().numpy(), kh[: int(oh[-1])]):
+            raise AssertionError("redis parse: key bytes differ from the generator's")
+    return {"workload": f"{nreq} pipelined RESP GETs over the first C2 keys", "stream_bytes": len(stream),
+            "ms_per_parse_wall": round(dt * 1e3, 4), "stream_gb_s": round(len(stream) / dt / 1e9, 2),
+            "mreq_s": round(nreq / dt / 1e6, 1)}
 
 
 if __name__ == "__main__":
