@@ -23,9 +23,9 @@
  *      start that is not '*': that request fails at its first byte
  *      (SW_START, :478-483), so an ok chain that stops short of the stream
  *      end is followed by one failing request;
- *   2. one thread per candidate runs the request state machine from there:
- *      status, end, key count. Bulk data is skipped by its length, so a
- *      thread touches O(tokens) bytes, not O(bytes);
+ *   2. one thread per candidate runs the request state machine from there,
+ *      one bulk string per step: status, end, key count. Bulk data is
+ *      skipped by its length, so a thread touches O(tokens) bytes;
  *   3. next[c] = the candidate at c's end (binary search), or none when c
  *      failed, is incomplete or ends the stream;
  *   4. the chain from candidate 0 is marked by radix-4 pointer jumping
@@ -96,139 +96,135 @@ __device__ uint8_t cmd_class(const uint8_t *__restrict__ m, uint32_t len)
 
 constexpr int32_t kIncomplete = 1; /* the request runs past the stream end */
 
-enum { RS_NARG, RS_NARG_LF, RS_TYPE_LEN, RS_TYPE_LEN_LF, RS_TYPE, RS_TYPE_LF, RS_KEY_LEN, RS_KEY_LEN_LF,
-       RS_KEY, RS_KEY_LF, RS_ARG_LEN, RS_ARG_LEN_LF, RS_ARG, RS_ARG_LF };
+enum BulkKind { BK_TYPE, BK_KEY, BK_ARG };
 
-/* One request from s[p0]: the state machine of redis_parse_req for the key
- * classes. Returns the status; on 0, *end is one past its LF and *nkeys its
- * key count. EMIT writes each key's span at base + i; the count pass writes
- * the first key's span to *kstart, *klen. */
+/* One bulk string "$<len>\r\n<data>\r\n" from s[*pp]: SW_REQ_TYPE_LEN /
+ * SW_KEY_LEN / SW_ARG*_LEN (:523-543, :1362-1389, :1492-1512, :1807-1825),
+ * their LF states, the data and its CR (:557-, :1403-1435, :1526-1544), and
+ * the LF after it. The checks run in the reference's byte order, so the first
+ * failure (or the stream end) gives the same status as the byte machine. On
+ * 0, *pp is past the LF, the data is s[*dp, *dp + *dl) and *cls the command
+ * class (BK_TYPE). */
+__device__ __forceinline__ int32_t bulk(const uint8_t *__restrict__ s, uint32_t n, uint32_t *pp, BulkKind kind,
+                                        uint32_t max_key_len, uint32_t *rnarg, uint32_t *dp, uint32_t *dl,
+                                        uint8_t *cls)
+{
+    const uint32_t token = *pp;
+    if (token >= n) return kIncomplete;
+    if (s[token] != '$') return NC_GPUHASH_REDIS_EINVAL;
+    uint32_t q = token + 1, rlen = 0;
+    for (;;) {
+        if (q >= n) return kIncomplete;
+        const uint8_t ch = s[q];
+        if (ch >= '0' && ch <= '9') {
+            rlen = rlen * 10u + (uint32_t)(ch - '0');
+            q++;
+            continue;
+        }
+        if (ch == '\r') break;
+        return NC_GPUHASH_REDIS_EINVAL;
+    }
+    if (kind == BK_TYPE && (rlen == 0 || *rnarg == 0)) return NC_GPUHASH_REDIS_EINVAL;
+    if (kind == BK_KEY && rlen >= max_key_len) return NC_GPUHASH_REDIS_EKEYLEN;
+    if (kind == BK_KEY && *rnarg == 0) return NC_GPUHASH_REDIS_EINVAL;
+    if (kind == BK_ARG && (q - token <= 1 || *rnarg == 0)) return NC_GPUHASH_REDIS_EINVAL;
+    (*rnarg)--;
+    if (q + 1 >= n) return kIncomplete;
+    if (s[q + 1] != '\n') return NC_GPUHASH_REDIS_EINVAL;
+    const uint32_t d = q + 2;
+    if (d >= n) return kIncomplete;
+    const uint64_t m = (uint64_t)d + rlen; /* rlen data bytes, then CR */
+    if (m >= n) return kIncomplete;
+    if (s[m] != '\r') return NC_GPUHASH_REDIS_EINVAL;
+    if (kind == BK_TYPE) {
+        *cls = cmd_class(s + d, rlen);
+        if (*cls == RC_NONE) return NC_GPUHASH_REDIS_EUNSUPPORTED;
+    }
+    if (m + 1 >= n) return kIncomplete;
+    if (s[m + 1] != '\n') return NC_GPUHASH_REDIS_EINVAL;
+    *pp = (uint32_t)m + 2u;
+    *dp = d;
+    *dl = rlen;
+    return NC_GPUHASH_REDIS_OK;
+}
+
+/* One request from s[p0]: redis_parse_req for the key classes, one bulk
+ * string per step (lanes parsing same-shaped requests stay converged).
+ * Returns the status; on 0, *end is one past its LF and *nkeys its key count.
+ * EMIT writes each key's span at base + i; the count pass writes the first
+ * key's span to *kstart, *klen. oracle_redis_parse is the byte-at-a-time
+ * restatement it is tested against. */
 template <bool EMIT>
 __device__ int32_t parse_req(const uint8_t *__restrict__ s, uint32_t n, uint32_t p0, uint32_t max_key_len,
                              uint32_t *end, uint32_t *nkeys, uint32_t *kstart, uint32_t *klen, uint32_t *kreq,
                              uint32_t base, uint32_t req)
 {
     if (s[p0] != '*') return NC_GPUHASH_REDIS_EINVAL; /* SW_START (:478-483) */
-    uint32_t narg = 0, rnarg = 0, rlen = 0, kn = 0, token = 0;
-    int state = RS_NARG;
-    uint8_t cls = RC_NONE;
-    bool have_token = false;
-    /* p advances at the bottom: by one byte, or past a bulk string (next_p).
-     * Assigning the for-loop counter inside the switch instead was
-     * miscompiled for gfx950 (the skip was lost; found by the parity tests). */
-    for (uint32_t p = p0 + 1, next_p; p < n; p = next_p) {
+    uint32_t p = p0 + 1, rnarg = 0;
+    for (;;) { /* SW_NARG (:492-509) */
+        if (p >= n) return kIncomplete;
         const uint8_t ch = s[p];
-        next_p = p + 1;
-        switch (state) {
-        case RS_NARG:
-            if (ch >= '0' && ch <= '9') rnarg = rnarg * 10u + (uint32_t)(ch - '0');
-            else if (ch == '\r' && rnarg != 0) { narg = rnarg; state = RS_NARG_LF; }
-            else return NC_GPUHASH_REDIS_EINVAL;
-            break;
-        case RS_NARG_LF:
-        case RS_TYPE_LEN_LF:
-        case RS_KEY_LEN_LF:
-        case RS_ARG_LEN_LF:
-            if (ch != '\n') return NC_GPUHASH_REDIS_EINVAL;
-            state = state == RS_NARG_LF ? RS_TYPE_LEN : state == RS_TYPE_LEN_LF ? RS_TYPE
-                  : state == RS_KEY_LEN_LF ? RS_KEY : RS_ARG;
-            have_token = false;
-            break;
-        case RS_TYPE_LEN:
-        case RS_KEY_LEN:
-        case RS_ARG_LEN:
-            if (!have_token) {
-                if (ch != '$') return NC_GPUHASH_REDIS_EINVAL;
-                have_token = true;
-                token = p;
-                rlen = 0;
-            } else if (ch >= '0' && ch <= '9') {
-                rlen = rlen * 10u + (uint32_t)(ch - '0');
-            } else if (ch == '\r') {
-                if (state == RS_TYPE_LEN && (rlen == 0 || rnarg == 0)) return NC_GPUHASH_REDIS_EINVAL;
-                if (state == RS_KEY_LEN && rlen >= max_key_len) return NC_GPUHASH_REDIS_EKEYLEN;
-                if (state == RS_KEY_LEN && rnarg == 0) return NC_GPUHASH_REDIS_EINVAL;
-                if (state == RS_ARG_LEN && (p - token <= 1 || rnarg == 0)) return NC_GPUHASH_REDIS_EINVAL;
-                rnarg--;
-                state = state == RS_TYPE_LEN ? RS_TYPE_LEN_LF : state == RS_KEY_LEN ? RS_KEY_LEN_LF : RS_ARG_LEN_LF;
-            } else {
-                return NC_GPUHASH_REDIS_EINVAL;
-            }
-            break;
-        case RS_TYPE:
-        case RS_KEY:
-        case RS_ARG: {
-            const uint64_t m = (uint64_t)p + rlen; /* rlen data bytes, then CR */
-            if (m >= n) return kIncomplete;
-            if (s[m] != '\r') return NC_GPUHASH_REDIS_EINVAL;
-            if (state == RS_TYPE) {
-                cls = cmd_class(s + p, rlen);
-                if (cls == RC_NONE) return NC_GPUHASH_REDIS_EUNSUPPORTED;
-                state = RS_TYPE_LF;
-            } else if (state == RS_KEY) {
-                if constexpr (EMIT) {
-                    kstart[base + kn] = p;
-                    klen[base + kn] = rlen;
-                    kreq[base + kn] = req;
-                } else if (kn == 0) { /* count pass: the first key's span in *kstart, *klen */
-                    *kstart = p;
-                    *klen = rlen;
-                }
-                kn++;
-                state = RS_KEY_LF;
-            } else {
-                state = RS_ARG_LF;
-            }
-            next_p = (uint32_t)m + 1u;
-            break;
+        if (ch >= '0' && ch <= '9') {
+            rnarg = rnarg * 10u + (uint32_t)(ch - '0');
+            p++;
+            continue;
         }
-        case RS_TYPE_LF:
-            if (ch != '\n' || narg == 1) return NC_GPUHASH_REDIS_EINVAL;
-            state = RS_KEY_LEN;
-            have_token = false;
-            break;
-        case RS_KEY_LF: {
-            if (ch != '\n') return NC_GPUHASH_REDIS_EINVAL;
-            have_token = false;
-            bool fin = false;
+        if (ch == '\r' && rnarg != 0) break;
+        return NC_GPUHASH_REDIS_EINVAL;
+    }
+    const uint32_t narg = rnarg;
+    if (p + 1 >= n) return kIncomplete; /* SW_NARG_LF */
+    if (s[p + 1] != '\n') return NC_GPUHASH_REDIS_EINVAL;
+    p += 2;
+    uint32_t dp = 0, dl = 0, kn = 0;
+    uint8_t cls = RC_NONE;
+    int32_t st = bulk(s, n, &p, BK_TYPE, max_key_len, &rnarg, &dp, &dl, &cls);
+    if (st != NC_GPUHASH_REDIS_OK) return st;
+    if (narg == 1) return NC_GPUHASH_REDIS_EINVAL; /* SW_REQ_TYPE_LF (:1347-1348) */
+    BulkKind kind = BK_KEY;
+    for (;;) {
+        st = bulk(s, n, &p, kind, max_key_len, &rnarg, &dp, &dl, &cls);
+        if (st != NC_GPUHASH_REDIS_OK) return st;
+        bool fin = false;
+        if (kind == BK_KEY) { /* SW_KEY_LF (:1437-1490) */
+            if constexpr (EMIT) {
+                kstart[base + kn] = dp;
+                klen[base + kn] = dl;
+                kreq[base + kn] = req;
+            } else if (kn == 0) {
+                *kstart = dp;
+                *klen = dl;
+            }
+            kn++;
             if (cls == RC_ARG0) {
                 if (rnarg != 0) return NC_GPUHASH_REDIS_EINVAL;
                 fin = true;
             } else if (cls == RC_ARG1) {
                 if (rnarg != 1) return NC_GPUHASH_REDIS_EINVAL;
-                state = RS_ARG_LEN;
+                kind = BK_ARG;
             } else if (cls == RC_ARGN || cls == RC_ARGX) {
                 if (rnarg == 0) fin = true;
-                else state = cls == RC_ARGX ? RS_KEY_LEN : RS_ARG_LEN;
+                else kind = cls == RC_ARGX ? BK_KEY : BK_ARG;
             } else { /* argkvx */
                 if (narg % 2 == 0) return NC_GPUHASH_REDIS_EINVAL;
-                state = RS_ARG_LEN;
+                kind = BK_ARG;
             }
-            if (fin) {
-                *end = p + 1;
-                *nkeys = kn;
-                return NC_GPUHASH_REDIS_OK;
-            }
-            break;
-        }
-        case RS_ARG_LF:
-            if (ch != '\n') return NC_GPUHASH_REDIS_EINVAL;
-            have_token = false;
+        } else { /* SW_ARG1_LF (:1546-1589), SW_ARGN_LF (:1858-1878) */
             if (cls == RC_ARG1) {
                 if (rnarg != 0) return NC_GPUHASH_REDIS_EINVAL;
-                *end = p + 1;
-                *nkeys = kn;
-                return NC_GPUHASH_REDIS_OK;
-            } else if (rnarg == 0) { /* argn, argkvx */
-                *end = p + 1;
-                *nkeys = kn;
-                return NC_GPUHASH_REDIS_OK;
+                fin = true;
+            } else if (rnarg == 0) {
+                fin = true;
+            } else {
+                kind = cls == RC_ARGN ? BK_ARG : BK_KEY;
             }
-            state = cls == RC_ARGN ? RS_ARG_LEN : RS_KEY_LEN;
-            break;
+        }
+        if (fin) {
+            *end = p;
+            *nkeys = kn;
+            return NC_GPUHASH_REDIS_OK;
         }
     }
-    return kIncomplete;
 }
 
 /* Candidate starts (position 0, or '*' right after CR LF) of the 16-B aligned
