@@ -152,9 +152,24 @@ def load_traffic(kernel_mode: str, workload: str):
     return best
 
 
-def cpu_baseline(t, spec, n, mode_names, reps=3):
+def online_cores() -> int:
+    """sysconf(_SC_NPROCESSORS_ONLN), bounded by this process's CPU affinity
+    (SURVEY.md §8d / BASELINE.md: all online host cores)."""
+    n = os.sysconf("SC_NPROCESSORS_ONLN")
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    return max(1, min(int(n), 256))  # oracle/ref_driver.c runs at most 256 pthreads
+
+
+def cpu_baseline(t, spec, n, mode_names, reps=5):
     """Reference hashkit (oracle/_ref, compiled from /root/reference) or, when
-    that build is absent, the repo's C restatement, timed on this host."""
+    that build is absent, the repo's C restatement, timed on this host: one
+    thread, and every online core (best of `reps` after a warm-up, per-key
+    hash_t calls over byte-balanced contiguous ranges, BASELINE.md:40-44).
+    The figure at the job's own CPU share (OMP_NUM_THREADS, 16 on the GPU
+    box) is reported beside it."""
     from tests.oracle_lib import Oracle, RefHashkit
 
     if RefHashkit.available():
@@ -163,15 +178,17 @@ def cpu_baseline(t, spec, n, mode_names, reps=3):
         impl, kind = Oracle(), "port"
     keys, off = t.synth_host(spec, 0, n)
     nbytes = int(off[-1])
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    cores = online_cores()
+    share = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or cores))
     res = {}
     for name in mode_names:
         m = t.HASH_NAMES.index(name)
-        s1 = impl.time_batch(m, keys, off, 1, reps)
-        sN = impl.time_batch(m, keys, off, threads, reps)
-        res[name] = {"mkeys_s_1thread": round(n / s1 / 1e6, 2), "gbs_1thread": round(nbytes / s1 / 1e9, 3),
-                     f"mkeys_s_{threads}threads": round(n / sN / 1e6, 2),
-                     f"gbs_{threads}threads": round(nbytes / sN / 1e9, 3)}
+        r = {}
+        for th in sorted({1, share, cores}):
+            s = impl.time_batch(m, keys, off, th, reps)
+            r[f"mkeys_s_{th}threads"] = round(n / s / 1e6, 2)
+            r[f"gbs_{th}threads"] = round(nbytes / s / 1e9, 3)
+        res[name] = r
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -181,11 +198,12 @@ def cpu_baseline(t, spec, n, mode_names, reps=3):
     except OSError:
         pass
     head = res[mode_names[0]]
-    return {"value": head[f"mkeys_s_{threads}threads"], "unit": "Mkeys/s", "cores": threads, "kind": kind,
+    return {"value": head[f"mkeys_s_{cores}threads"], "unit": "Mkeys/s", "cores": cores, "kind": kind,
             "sample": f"first {n} keys of the same workload ({nbytes} key bytes), {mode_names[0]}, "
-                      f"best of {reps} after a warm-up, per-key hash_t calls on {threads} pthreads over "
-                      f"byte-balanced ranges; single-thread and md5 alongside",
-            "cpu_model": cpu_model, "detail": res}
+                      f"best of {reps} after a warm-up, per-key hash_t calls on {cores} pthreads (all online "
+                      f"cores) over byte-balanced ranges; 1 thread, the job's {share}-thread CPU share and md5 "
+                      f"alongside",
+            "threads_share": share, "cpu_model": cpu_model, "detail": res}
 
 
 def main():

@@ -180,9 +180,11 @@ void nc_gpuhash_mc_parser_destroy(nc_gpuhash_mc_parser_t *ps);
 /* Parse d_stream[0, nbytes). Writes the packed keys (d_keys, NULL = spans
  * only; needs result->nkeys's bytes + NC_GPUHASH_PAD), d_offsets (nkeys + 1),
  * the request index of each key (d_key_req, may be NULL) and each request's
- * NC_GPUHASH_MC_* status (d_req_status, nreqs entries, may be NULL). Blocks
- * until done (the counts size the next launch). NC_ENOMEM when a limit of the
- * workspace is exceeded. */
+ * NC_GPUHASH_MC_* status (d_req_status, room for max_reqs entries, may be
+ * NULL). Blocks until done (the counts size the next launch). NC_ENOMEM when
+ * a limit of the workspace is exceeded (more complete request lines than
+ * max_reqs, more keys than max_keys, or more than max_bytes), with nothing
+ * written past those limits. */
 rstatus_t nc_gpuhash_mc_parse_device(nc_gpuhash_mc_parser_t *ps, const uint8_t *d_stream, uint64_t nbytes,
                                      uint8_t *d_keys, uint64_t *d_offsets, uint32_t *d_key_req,
                                      int32_t *d_req_status, struct nc_gpuhash_mc_result *result,
@@ -217,46 +219,14 @@ void nc_gpuhash_redis_parser_destroy(nc_gpuhash_redis_parser_t *ps);
 
 /* Parse d_stream[0, nbytes); max_key_len is mbuf_data_size() (keys must be
  * shorter). Outputs as nc_gpuhash_mc_parse_device, with NC_GPUHASH_REDIS_*
- * statuses. Blocks until done. */
+ * statuses; d_req_status holds max_reqs entries. A stream of max_reqs ok
+ * requests followed by a byte that starts no request is accepted: nreqs then
+ * counts the failing request (max_reqs + 1) and first_error names it, but its
+ * status has no slot and is not written. Blocks until done. */
 rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps, const uint8_t *d_stream, uint64_t nbytes,
                                         uint32_t max_key_len, uint8_t *d_keys, uint64_t *d_offsets,
                                         uint32_t *d_key_req, int32_t *d_req_status,
                                         struct nc_gpuhash_redis_result *result, void *stream);
-
-/* The launch variant the auto policy picks for this mode and shape (the
- * variant bits of nc_gpuhash_set_tuning; bit 16 = the plain workgroup
- * pipeline); -1 with errno EINVAL for an invalid mode. */
-int nc_gpuhash_pick_variant(int mode, uint64_t nkeys, const struct nc_gpuhash_shape *shape);
-
-/* Same launch repeated `iters` times between two hipEvents recorded on
- * `stream`; blocks until done and stores the mean milliseconds per launch. */
-rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
-                                 uint64_t nkeys, uint32_t *d_out, void *stream,
-                                 int iters, float *avg_ms);
-rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
-                                        uint64_t nkeys, uint32_t *d_out,
-                                        const struct nc_gpuhash_shape *shape, void *stream,
-                                        int iters, float *avg_ms);
-
-/* Launch tuning (process-wide; for tests and benchmarks; every setting gives
- * identical outputs; variant 0 = the shape-driven auto policy, any other
- * value is used as given). grid_cap: maximum workgroups per launch (0 = persistent,
- * one per resident slot; -1 = keep). sort: group a tile's keys by length
- * before hashing (1 on, 0 off, -1 keep). variant: kernel code variant bits
- * (bit 0: shift-add FNV-64 multiply; bit 3: DIAGNOSTIC no-hash build,
- * fnv1a_64 unsorted only, outputs are NOT hashes, with bits 1-2 its L2
- * prefetch distance code (0 off, 1..3 = 2..4 tiles ahead); bit 4: DIAGNOSTIC arithmetic offsets
- * for fixed 32-byte keys, fnv1a_64 unsorted only; bit 5: register-staged
- * pipeline, two tiles in flight; bit 6: default cache policy on the key,
- * offset and output streams instead of non-temporal, fnv1a_64 and md5 only;
- * bit 7: wave-ring pipeline, bits 8-10 its slab/look-ahead shape; bits 11-15:
- * wave-ring options (fnv1a_64, md5: 4 waves per workgroup, pair-interleaved
- * keys, 64-key tiles, 256-key tiles hashed in length-sorted rounds, 128-key
- * tiles in two sorted rounds); bit 16: the plain workgroup
- * pipeline as an explicit choice; bit 17: length-grouped tiles, as sort = 1;
- * bit 18: workgroup pipelines launch three resident sets of workgroups;
- * -1 = keep). */
-rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
 /* ---- 3b. host batches through a context (pinned staging, one stream per slot) ---- */
 typedef struct nc_gpuhash_ctx nc_gpuhash_ctx_t;

@@ -1,8 +1,12 @@
 /*
- * Diagnostics: a STREAM-style read kernel that measures the achievable HBM
- * read bandwidth in the same run as the hash kernels (SURVEY.md §8d asks for
- * the roofline fraction against both the 8 TB/s spec and a measured
- * read ceiling). Not part of the hashing path.
+ * Diagnostics and benchmark tuning — NOT part of the drop-in boundary
+ * (include/nc_gpuhash.h is). A proxy never needs these:
+ *   - a STREAM-style read kernel that measures the achievable HBM read
+ *     bandwidth in the same run as the hash kernels (SURVEY.md §8d asks for
+ *     the roofline fraction against both the 8 TB/s spec and a measured read
+ *     ceiling);
+ *   - the shape policy's kernel choice, an event-timed launch loop, and the
+ *     process-wide launch tuning used by tests and sweeps.
  */
 #ifndef NC_GPUHASH_PROBE_H
 #define NC_GPUHASH_PROBE_H
@@ -24,6 +28,41 @@ rstatus_t nc_gpuhash_probe_read(const void *d_buf, uint64_t bytes, uint32_t *d_s
  * under the cache policy of launch variant bit 6. */
 rstatus_t nc_gpuhash_probe_read_nt(const void *d_buf, uint64_t bytes, uint32_t *d_sink, void *stream, int iters,
                                    float *avg_ms);
+
+/* The launch variant the auto policy picks for this mode and shape (the
+ * variant bits of nc_gpuhash_set_tuning; bit 16 = the plain workgroup
+ * pipeline); -1 with errno EINVAL for an invalid mode. */
+int nc_gpuhash_pick_variant(int mode, uint64_t nkeys, const struct nc_gpuhash_shape *shape);
+
+/* Same launch repeated `iters` times between two hipEvents recorded on
+ * `stream`; blocks until done and stores the mean milliseconds per launch. */
+rstatus_t nc_gpuhash_time_device(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
+                                 uint64_t nkeys, uint32_t *d_out, void *stream,
+                                 int iters, float *avg_ms);
+rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
+                                        uint64_t nkeys, uint32_t *d_out,
+                                        const struct nc_gpuhash_shape *shape, void *stream,
+                                        int iters, float *avg_ms);
+
+/* Launch tuning (process-wide, atomic; for tests and benchmarks only; every setting gives
+ * identical outputs; variant 0 = the shape-driven auto policy, any other
+ * value is used as given). grid_cap: maximum workgroups per launch (0 = persistent,
+ * one per resident slot; -1 = keep). sort: group a tile's keys by length
+ * before hashing (1 on, 0 off, -1 keep). variant: kernel code variant bits
+ * (bit 0: shift-add FNV-64 multiply; bit 3: DIAGNOSTIC no-hash build,
+ * fnv1a_64 unsorted only, outputs are NOT hashes, with bits 1-2 its L2
+ * prefetch distance code (0 off, 1..3 = 2..4 tiles ahead); bit 4: DIAGNOSTIC arithmetic offsets
+ * for fixed 32-byte keys, fnv1a_64 unsorted only; bit 5: register-staged
+ * pipeline, two tiles in flight; bit 6: default cache policy on the key,
+ * offset and output streams instead of non-temporal, fnv1a_64 and md5 only;
+ * bit 7: wave-ring pipeline, bits 8-10 its slab/look-ahead shape; bits 11-15:
+ * wave-ring options (fnv1a_64, md5: 4 waves per workgroup, pair-interleaved
+ * keys, 64-key tiles, 256-key tiles hashed in length-sorted rounds, 128-key
+ * tiles in two sorted rounds); bit 16: the plain workgroup
+ * pipeline as an explicit choice; bit 17: length-grouped tiles, as sort = 1;
+ * bit 18: workgroup pipelines launch three resident sets of workgroups;
+ * -1 = keep). */
+rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
 #ifdef __cplusplus
 }

@@ -213,3 +213,31 @@ def test_redis_parser_argument_errors():
         assert not lib.nc_gpuhash_redis_parser_create(*args)
         assert ctypes.get_errno() == errno.EINVAL
     assert lib.nc_gpuhash_redis_parse_device(None, None, 0, 16336, None, None, None, None, None, None) == L.NC_ERROR
+
+
+def test_device_entry_points_check_their_arguments():
+    """The Python mirror rejects what would fault or misread on the device
+    before any call reaches the C ABI (host tensors, wrong dtypes, a key buffer
+    without NC_GPUHASH_PAD readable bytes past offsets[-1])."""
+    import torch
+
+    keys = torch.zeros(64, dtype=torch.uint8)
+    off = torch.tensor([0, 8, 16], dtype=torch.int64)
+    with pytest.raises(ValueError, match="CUDA"):
+        t.hash_batch_device("fnv1a_64", keys, off)
+    with pytest.raises(TypeError):
+        t.hash_batch_device("fnv1a_64", keys.int(), off)
+    from twemproxy_amd.hashkit import _check_stream
+
+    # 40 bytes of keys cannot hold offsets[-1] = 16 plus NC_GPUHASH_PAD = 32 readable bytes
+    with pytest.raises(ValueError, match="NC_GPUHASH_PAD"):
+        t.hash_batch_device("fnv1a_64", torch.zeros(40, dtype=torch.uint8), off, key_end=16)
+    with pytest.raises(ValueError, match="NC_GPUHASH_PAD"):
+        t.server_idx_device("fnv1a_64", "ketama", torch.zeros(47, dtype=torch.uint8), off,
+                            torch.zeros((4, 2), dtype=torch.int32), 2, key_end=16)
+    with pytest.raises(ValueError, match="CUDA"):  # enough room: then residency is the error
+        t.hash_batch_device("fnv1a_64", torch.zeros(48, dtype=torch.uint8), off, key_end=16)
+    with pytest.raises(ValueError, match="CUDA"):
+        _check_stream(torch.zeros(8, dtype=torch.uint8))
+    with pytest.raises(TypeError):
+        _check_stream(torch.zeros(8, dtype=torch.int16))

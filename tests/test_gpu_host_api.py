@@ -95,3 +95,39 @@ def test_context_zero_copy(gpu, oracle, zc):
                 tk, out = ctx.submit(m, k, o)
                 ctx.wait(tk)
                 np.testing.assert_array_equal(out, oracle.batch(m, k, o), err_msg=f"n={n} mode={m}")
+
+
+def test_context_shared_by_worker_threads(gpu, oracle):
+    """one context, 4 threads each submitting and polling its
+    own batches (slot state is under the context's lock). Every output must be
+    delivered to its own batch exactly, whichever thread recycles the slot."""
+    import threading
+
+    batches = [t.synth_host(t.SynthSpec.zipf(100 + i), 0, 700 + 37 * i) for i in range(4 * 12)]
+    want = [oracle.batch(6 if i % 2 == 0 else 1, k, o) for i, (k, o) in enumerate(batches)]
+    errors = []
+    with t.Context(max_keys=4096, max_key_bytes=1 << 18, nslots=3) as ctx:
+        def worker(w):
+            try:
+                for j in range(w, len(batches), 4):
+                    k, o = batches[j]
+                    while True:
+                        try:
+                            tk, out = ctx.submit("fnv1a_64" if j % 2 == 0 else "md5", k, o)
+                            break
+                        except BlockingIOError:
+                            pass
+                    while not ctx.poll(tk):
+                        pass
+                    if not np.array_equal(out, want[j]):
+                        errors.append(j)
+            except Exception as e:  # reported below, never swallowed
+                errors.append(repr(e))
+
+        threads = [threading.Thread(target=worker, args=(w,)) for w in range(4)]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join(120)
+        assert not any(th.is_alive() for th in threads)
+    assert errors == []

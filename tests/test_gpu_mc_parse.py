@@ -105,3 +105,32 @@ def test_extracted_keys_hash_like_the_host(gpu, oracle, parser):
         h = t.hash_batch_device(name, kd, od)
         torch.cuda.synchronize()
         assert h.cpu().numpy().view(np.uint32).tolist() == [t.hash_key(name, k) for k in keys], name
+
+
+def test_more_lines_than_max_reqs(gpu):
+    """More CR LF lines than max_reqs (data lines of a storage command, or a
+    max_reqs sized to the expected requests): NC_ENOMEM, and the LF select
+    must not write past its buffer (it is sized from max_bytes)."""
+    import torch
+
+    stream = b"get a\r\n" * 16 + b"x\r\n" * 300
+    with t.McParser(max_bytes=4096, max_reqs=8, max_keys=64) as p:
+        with pytest.raises(t.NcError):
+            p.parse(dev(stream))
+        torch.cuda.synchronize()
+        # the workspace is intact afterwards
+        _, off, _, _, info = p.parse(dev(b"get a bb\r\nget c\r\n"))
+        torch.cuda.synchronize()
+        assert info["nkeys"] == 3 and off.cpu().tolist() == [0, 1, 3, 4]
+
+
+def test_parser_rejects_host_and_mistyped_streams(gpu):
+    import torch
+
+    with t.McParser(max_bytes=1024, max_reqs=8, max_keys=8) as p:
+        with pytest.raises(ValueError):
+            p.parse(torch.zeros(16, dtype=torch.uint8))  # host memory
+        with pytest.raises(TypeError):
+            p.parse(torch.zeros(16, dtype=torch.int32, device="cuda"))
+        with pytest.raises(ValueError):
+            p.parse(torch.zeros(32, dtype=torch.uint8, device="cuda")[::2])

@@ -140,6 +140,17 @@ def test_limits(gpu, oracle):
         _, off, _, _, info = p.parse(dev(b"*3\r\n$3\r\ndel\r\n$1\r\na\r\n$1\r\nb\r\n"))
         torch.cuda.synchronize()
         assert info["nkeys"] == 2 and off.cpu().tolist() == [0, 1, 2]
+    # exactly max_reqs ok requests, then a byte that starts no request: the
+    # synthetic failing request does not count against max_reqs
+    get = b"*2\r\n$3\r\nget\r\n$1\r\na\r\n"
+    with t.RedisParser(max_bytes=256, max_reqs=4, max_keys=4) as p:
+        _, off, _, status, info = p.parse(dev(get * 4 + b"x"))
+        torch.cuda.synchronize()
+        assert info["nkeys"] == 4 and info["first_error"] == 4 and info["nreqs"] == 5, info
+        assert info["consumed"] == 4 * len(get)
+        assert status.cpu().tolist() == [0, 0, 0, 0]
+        _, _, _, oi = oracle.redis_parse(get * 4 + b"x")[1:]
+        assert (oi["nkeys"], oi["first_error"], oi["consumed"]) == (4, 4, 4 * len(get)), oi
 
 
 def test_extracted_keys_hash_like_the_host(gpu, oracle, parser):

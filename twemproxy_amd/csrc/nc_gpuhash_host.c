@@ -113,9 +113,11 @@ struct nc_slot {
     uint32_t *d_out;
     uint32_t *user_out;
     uint32_t nkeys;
-    int busy;
+    int busy; /* SLOT_FREE, SLOT_PACKING (owned by one submitter, not yet launched), SLOT_RUNNING */
     int ticket;
 };
+
+enum { SLOT_FREE = 0, SLOT_PACKING = 1, SLOT_RUNNING = 2 };
 
 struct nc_gpuhash_ctx {
     int device;
@@ -126,6 +128,12 @@ struct nc_gpuhash_ctx {
     uint64_t zero_copy_bytes; /* batches with at most this many key bytes skip the copies */
     int unmapped;             /* staging has no device mapping: zero-copy unavailable */
     struct nc_slot *slots;
+    /* Slot state (busy, ticket, user_out, next_gen) is shared by every thread
+     * that submits to or polls this context (the batch layer
+     * must be safe from worker threads). A slot being packed is owned by its
+     * submitter alone, so the memcpy into pinned staging runs unlocked. */
+    pthread_mutex_t lock;
+    int lock_init;
 };
 
 static rstatus_t hip_fail(hipError_t e)
@@ -156,6 +164,7 @@ void nc_gpuhash_ctx_destroy(nc_gpuhash_ctx_t *ctx)
         }
         free(ctx->slots);
     }
+    if (ctx->lock_init) pthread_mutex_destroy(&ctx->lock);
     free(ctx);
 }
 
@@ -175,6 +184,12 @@ nc_gpuhash_ctx_t *nc_gpuhash_ctx_create(int device, uint64_t max_keys, uint64_t 
         errno = ENOMEM;
         return NULL;
     }
+    if (pthread_mutex_init(&ctx->lock, NULL) != 0) {
+        free(ctx);
+        errno = ENOMEM;
+        return NULL;
+    }
+    ctx->lock_init = 1;
     ctx->device = device;
     ctx->max_keys = max_keys;
     ctx->max_key_bytes = max_key_bytes;
@@ -225,62 +240,85 @@ rstatus_t nc_gpuhash_ctx_set_zero_copy(nc_gpuhash_ctx_t *ctx, uint64_t max_key_b
         errno = EINVAL;
         return NC_ERROR;
     }
+    pthread_mutex_lock(&ctx->lock);
     ctx->zero_copy_bytes = max_key_bytes;
+    pthread_mutex_unlock(&ctx->lock);
     return NC_OK;
 }
 
-/* Copy a finished slot's hashes to the caller and free the slot. */
+/* Copy a finished slot's hashes to the caller and free the slot (ctx->lock held). */
 static void slot_finish(struct nc_slot *s)
 {
     memcpy(s->user_out, s->h_out, (size_t)s->nkeys * sizeof(uint32_t));
-    s->busy = 0;
+    s->busy = SLOT_FREE;
 }
 
+/* A free slot, reserved for the caller (SLOT_PACKING); finished slots are
+ * delivered on the way. NULL when every slot is packing or still running. */
 static struct nc_slot *slot_acquire(nc_gpuhash_ctx_t *ctx, int *idx)
 {
+    struct nc_slot *got = NULL;
+    pthread_mutex_lock(&ctx->lock);
     for (int i = 0; i < ctx->nslots; i++) {
         struct nc_slot *s = &ctx->slots[i];
-        if (s->busy && hipEventQuery(s->done) == hipSuccess) {
+        if (s->busy == SLOT_RUNNING && hipEventQuery(s->done) == hipSuccess) {
             slot_finish(s);
         }
-        if (!s->busy) {
+        if (s->busy == SLOT_FREE) {
+            s->busy = SLOT_PACKING;
             *idx = i;
-            return s;
+            got = s;
+            break;
         }
     }
-    return NULL;
+    pthread_mutex_unlock(&ctx->lock);
+    return got;
 }
 
-/* Enqueue H2D -> kernel -> D2H on the slot's stream; staging already packed. */
+static rstatus_t slot_release(nc_gpuhash_ctx_t *ctx, struct nc_slot *s, rstatus_t rc)
+{
+    pthread_mutex_lock(&ctx->lock);
+    s->busy = SLOT_FREE;
+    pthread_mutex_unlock(&ctx->lock);
+    return rc;
+}
+
+/* Enqueue H2D -> kernel -> D2H on the slot's stream; staging already packed by
+ * the caller, who owns the slot (SLOT_PACKING). On failure the slot is freed. */
 static rstatus_t slot_launch(nc_gpuhash_ctx_t *ctx, struct nc_slot *s, int idx, int mode, uint32_t nkeys,
                              const struct nc_gpuhash_shape *shape, uint32_t *out, int *ticket)
 {
     const uint64_t nbytes = s->h_off[nkeys];
     memset(s->h_keys + nbytes, 0, NC_GPUHASH_PAD);
     hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(e);
-    if (nbytes <= ctx->zero_copy_bytes && !ctx->unmapped) {
+    if (e != hipSuccess) return slot_release(ctx, s, hip_fail(e));
+    pthread_mutex_lock(&ctx->lock);
+    const int zero_copy = nbytes <= ctx->zero_copy_bytes && !ctx->unmapped;
+    pthread_mutex_unlock(&ctx->lock);
+    if (zero_copy) {
         /* zero-copy: one kernel launch over the mapped staging, no DMA */
         if (nc_gpuhash_batch_device_shaped(mode, s->m_keys, s->m_off, nkeys, s->m_out, shape, s->stream) != NC_OK)
-            return NC_ERROR;
+            return slot_release(ctx, s, NC_ERROR);
     } else {
         e = hipMemcpyAsync(s->d_keys, s->h_keys, nbytes + NC_GPUHASH_PAD, hipMemcpyHostToDevice, s->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(s->d_off, s->h_off, ((size_t)nkeys + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
                                s->stream);
-        if (e != hipSuccess) return hip_fail(e);
+        if (e != hipSuccess) return slot_release(ctx, s, hip_fail(e));
         if (nc_gpuhash_batch_device_shaped(mode, s->d_keys, s->d_off, nkeys, s->d_out, shape, s->stream) != NC_OK)
-            return NC_ERROR;
+            return slot_release(ctx, s, NC_ERROR);
         e = hipMemcpyAsync(s->h_out, s->d_out, (size_t)nkeys * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream);
-        if (e != hipSuccess) return hip_fail(e);
+        if (e != hipSuccess) return slot_release(ctx, s, hip_fail(e));
     }
     e = hipEventRecord(s->done, s->stream);
-    if (e != hipSuccess) return hip_fail(e);
+    if (e != hipSuccess) return slot_release(ctx, s, hip_fail(e));
+    pthread_mutex_lock(&ctx->lock);
     s->user_out = out;
     s->nkeys = nkeys;
-    s->busy = 1;
     s->ticket = idx + ctx->nslots * (ctx->next_gen++ & 0xffffff);
+    s->busy = SLOT_RUNNING;
     *ticket = s->ticket;
+    pthread_mutex_unlock(&ctx->lock);
     return NC_OK;
 }
 
@@ -345,7 +383,7 @@ rstatus_t nc_gpuhash_submit_spans(nc_gpuhash_ctx_t *ctx, int mode, const struct 
         const size_t n = (size_t)(spans[i].end - spans[i].start);
         if (pos + n > ctx->max_key_bytes) {
             errno = ENOMEM;
-            return NC_ENOMEM;
+            return slot_release(ctx, s, NC_ENOMEM);
         }
         memcpy(s->h_keys + pos, spans[i].start, n);
         pos += n;
@@ -370,14 +408,16 @@ rstatus_t nc_gpuhash_poll(nc_gpuhash_ctx_t *ctx, int ticket)
         errno = EINVAL;
         return NC_ERROR;
     }
-    if (!s->busy || s->ticket != ticket) {
-        return NC_OK; /* finished and already delivered */
-    }
-    hipError_t e = hipEventQuery(s->done);
-    if (e == hipErrorNotReady) return NC_EAGAIN;
-    if (e != hipSuccess) return hip_fail(e);
-    slot_finish(s);
-    return NC_OK;
+    rstatus_t rc = NC_OK;
+    pthread_mutex_lock(&ctx->lock);
+    if (s->busy == SLOT_RUNNING && s->ticket == ticket) {
+        const hipError_t e = hipEventQuery(s->done);
+        if (e == hipErrorNotReady) rc = NC_EAGAIN;
+        else if (e != hipSuccess) rc = hip_fail(e);
+        else slot_finish(s);
+    } /* else finished and already delivered */
+    pthread_mutex_unlock(&ctx->lock);
+    return rc;
 }
 
 rstatus_t nc_gpuhash_wait(nc_gpuhash_ctx_t *ctx, int ticket)
@@ -387,10 +427,17 @@ rstatus_t nc_gpuhash_wait(nc_gpuhash_ctx_t *ctx, int ticket)
         errno = EINVAL;
         return NC_ERROR;
     }
-    if (!s->busy || s->ticket != ticket) return NC_OK;
+    pthread_mutex_lock(&ctx->lock);
+    const int pending = s->busy == SLOT_RUNNING && s->ticket == ticket;
+    pthread_mutex_unlock(&ctx->lock);
+    if (!pending) return NC_OK;
+    /* the event stays valid while the ticket's slot is not re-acquired, and a
+     * slot is re-acquired only after its event has completed */
     hipError_t e = hipEventSynchronize(s->done);
     if (e != hipSuccess) return hip_fail(e);
-    slot_finish(s);
+    pthread_mutex_lock(&ctx->lock);
+    if (s->busy == SLOT_RUNNING && s->ticket == ticket) slot_finish(s);
+    pthread_mutex_unlock(&ctx->lock);
     return NC_OK;
 }
 

@@ -31,6 +31,7 @@
 #include <stdlib.h>
 
 #include "nc_gpuhash.h"
+#include "nc_gpuhash_probe.h"
 #include "nc_hash_algo.h"
 
 namespace {
@@ -1635,7 +1636,8 @@ __global__ __launch_bounds__(256) void nc_dispatch_kernel(const uint32_t *__rest
 namespace nc_tu {
 extern int g_grid_cap; /* 0 = persistent: every resident workgroup slot once */
 extern int g_sort;     /* 1 on, 0 off */
-extern int g_variant;  /* variant bits, include/nc_gpuhash.h (nc_gpuhash_set_tuning) */
+extern int g_variant;  /* variant bits, include/nc_gpuhash_probe.h (nc_gpuhash_set_tuning) */
+/* the tuning globals are read and written with __atomic builtins (any thread) */
 extern int g_num_cus[64];
 
 /* one launch of mode MODE: the wave ring when var bit 7 is set (offsets
@@ -1676,35 +1678,44 @@ constexpr int kVarSorted = 1 << 17; /* group the tile's keys by length (the SORT
 constexpr int kVarRingSorted = 128 | 16384; /* 256-key wave tiles hashed in length-sorted rounds (6 KiB slots) */
 constexpr int kVarOver = 1 << 18; /* workgroup pipelines: three resident sets of workgroups per launch */
 
+int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
+
 int grid_cap()
 {
-    if (g_grid_cap < 0) {
+    int v = load_i(&g_grid_cap);
+    if (v < 0) {
         const char *e = getenv("NC_GPUHASH_GRID");
-        g_grid_cap = e ? atoi(e) : 0;
-        if (g_grid_cap < 0) g_grid_cap = 0;
+        v = e ? atoi(e) : 0;
+        if (v < 0) v = 0;
+        int unset = -1; /* an explicit nc_gpuhash_set_tuning wins over the environment */
+        if (!__atomic_compare_exchange_n(&g_grid_cap, &unset, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) v = unset;
     }
-    return g_grid_cap;
+    return v;
 }
 
 bool sort_enabled()
 {
-    if (g_sort < 0) {
+    int v = load_i(&g_sort);
+    if (v < 0) {
         const char *e = getenv("NC_GPUHASH_SORT");
-        g_sort = e ? (atoi(e) ? 1 : 0) : 0;
+        v = e ? (atoi(e) ? 1 : 0) : 0;
+        int unset = -1;
+        if (!__atomic_compare_exchange_n(&g_sort, &unset, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) v = unset;
     }
-    return g_sort == 1;
+    return v == 1;
 }
 
 int num_cus()
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (g_num_cus[dev] == 0) {
-        int n = 0;
+    int n = load_i(&g_num_cus[dev]);
+    if (n == 0) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        g_num_cus[dev] = n;
+        store_i(&g_num_cus[dev], n); /* every thread stores the same value */
     }
-    return g_num_cus[dev];
+    return n;
 }
 
 template <int MODE, bool SORT, int VAR>
@@ -2018,12 +2029,13 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
     const uintptr_t kp = reinterpret_cast<uintptr_t>(d_keys);
     const uint8_t *base = reinterpret_cast<const uint8_t *>(kp & ~(uintptr_t)15);
     const uint64_t delta = (uint64_t)(kp & 15u);
-    int var = g_variant != 0 ? g_variant : pick_variant(mode, nkeys, shape);
+    const int tuned = load_i(&g_variant);
+    int var = tuned != 0 ? tuned : pick_variant(mode, nkeys, shape);
     const bool sort = sort_enabled() || (var & kVarSorted) != 0;
     var &= ~(kVarWorkgroup | kVarSorted); /* kVarOver rides along to launch_kernel */
     /* the wave ring DMAs offsets 16 bytes per lane: it needs 16-byte aligned
      * offsets (any other alignment takes the workgroup pipeline) */
-    if ((var & 128) != 0 && (reinterpret_cast<uintptr_t>(d_off) & 15u) != 0) var = g_variant != 0 ? 0 : 32;
+    if ((var & 128) != 0 && (reinterpret_cast<uintptr_t>(d_off) & 15u) != 0) var = tuned != 0 ? 0 : 32;
     switch (mode) {
 #define NC_CASE(M) \
     case M: return nc_tu::entry<M>(base, d_off, delta, nkeys, d_out, stream, sort, var);
@@ -2132,9 +2144,9 @@ extern "C" int nc_gpuhash_pick_variant(int mode, uint64_t nkeys, const struct nc
 
 extern "C" rstatus_t nc_gpuhash_set_tuning(int grid_cap_, int sort, int variant)
 {
-    if (grid_cap_ >= 0) g_grid_cap = grid_cap_;
-    if (sort >= 0) g_sort = sort ? 1 : 0;
-    if (variant >= 0) g_variant = variant;
+    if (grid_cap_ >= 0) store_i(&g_grid_cap, grid_cap_);
+    if (sort >= 0) store_i(&g_sort, sort ? 1 : 0);
+    if (variant >= 0) store_i(&g_variant, variant);
     return NC_OK;
 }
 

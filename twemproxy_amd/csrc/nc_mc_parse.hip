@@ -204,7 +204,10 @@ extern "C" nc_gpuhash_mc_parser_t *nc_gpuhash_mc_parser_create(uint64_t max_byte
                                              (uint64_t *)nullptr, (int64_t)max_keys + 1);
     ps->tmp_bytes = t1 > t2 ? (t1 > t3 ? t1 : t3) : (t2 > t3 ? t2 : t3);
     if (e == hipSuccess) e = hipMalloc((void **)&ps->flag, max_bytes);
-    if (e == hipSuccess) e = hipMalloc((void **)&ps->lf, max_reqs * sizeof(uint64_t));
+    /* the LF select writes every CR LF of the stream before nreq can be
+     * checked against max_reqs: size it from the byte limit (one CR LF per
+     * two bytes at most), max_reqs only bounds what is reported */
+    if (e == hipSuccess) e = hipMalloc((void **)&ps->lf, (max_bytes / 2u + 1u) * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc((void **)&ps->status, max_reqs * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc((void **)&ps->nk, (max_reqs + 1) * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void **)&ps->kbase, (max_reqs + 1) * sizeof(uint64_t));

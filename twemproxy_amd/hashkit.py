@@ -131,7 +131,35 @@ def pick_variant(hash_: int | str, nkeys: int, shape=None) -> int:
     return v
 
 
-def hash_batch_device(hash_: int | str, keys, offsets, out=None, stream=None, shape=None):
+def _check_batch(keys, offsets, key_end=None) -> None:
+    """Argument checks of the device-resident entry points: uint8 keys, int64
+    offsets, both contiguous CUDA tensors, and a key buffer readable
+    NC_GPUHASH_PAD bytes past offsets[-1] (the kernels' vector reads run up to
+    that far). `key_end` is offsets[-1] as the packer knows it; when it is None
+    the value is read back from the device (one synchronising copy)."""
+    import torch
+
+    if keys.dtype != torch.uint8 or offsets.dtype != torch.int64:
+        raise TypeError("keys must be uint8 and offsets int64")
+    if not (keys.is_contiguous() and offsets.is_contiguous()):
+        raise ValueError("keys and offsets must be contiguous")
+    if offsets.dim() != 1 or offsets.numel() < 1:
+        raise ValueError("offsets must be a 1-D tensor of n+1 entries")
+    if offsets.numel() > 1 and key_end is not None:
+        _check_key_room(keys.numel(), int(key_end))
+    if not (keys.is_cuda and offsets.is_cuda):
+        raise ValueError("device entry points need CUDA (HIP) tensors")
+    if offsets.numel() > 1 and key_end is None:
+        _check_key_room(keys.numel(), int(offsets[-1].item()))
+
+
+def _check_key_room(nbytes: int, end: int) -> None:
+    if end < 0 or nbytes < end + L.NC_GPUHASH_PAD:
+        raise ValueError(f"keys holds {nbytes} bytes; offsets[-1] = {end} needs "
+                         f"{end + L.NC_GPUHASH_PAD} (NC_GPUHASH_PAD readable bytes past the last key)")
+
+
+def hash_batch_device(hash_: int | str, keys, offsets, out=None, stream=None, shape=None, key_end=None):
     """Device-resident batch on torch tensors.
 
     keys: uint8 CUDA tensor readable NC_GPUHASH_PAD bytes past offsets[-1];
@@ -139,20 +167,19 @@ def hash_batch_device(hash_: int | str, keys, offsets, out=None, stream=None, sh
     out: int32 CUDA tensor of n (allocated if None; the bits are the u32 hash).
     shape: optional (key_bytes, min_len, max_len) the packer knows, used only
     to pick the kernel pipeline (nc_gpuhash_batch_device_shaped).
+    key_end: offsets[-1] if the caller knows it (else it is read back from
+    the device once, to check the key buffer's size).
     Enqueued on `stream` (default: torch's current stream).
     """
     import torch
 
     mode = mode_of(hash_)
     n = offsets.numel() - 1
-    if keys.dtype != torch.uint8 or offsets.dtype != torch.int64:
-        raise TypeError("keys must be uint8 and offsets int64")
-    if not (keys.is_cuda and offsets.is_cuda):
-        raise ValueError("hash_batch_device needs CUDA (HIP) tensors")
-    if not (keys.is_contiguous() and offsets.is_contiguous()):
-        raise ValueError("keys and offsets must be contiguous")
+    _check_batch(keys, offsets, key_end)
     if out is None:
         out = torch.empty(max(n, 0), dtype=torch.int32, device=keys.device)
+    elif out.dtype != torch.int32 or not out.is_cuda or not out.is_contiguous() or out.numel() < n:
+        raise ValueError("out must be a contiguous int32 CUDA tensor of at least n entries")
     L.check(
         L.lib().nc_gpuhash_batch_device_shaped(
             mode, keys.data_ptr(), offsets.data_ptr(), n, out.data_ptr(), _shape_arg(shape), _stream_handle(stream)
@@ -184,7 +211,7 @@ def ketama_build_device(names: Sequence[bytes], weights: Sequence[int], live: Se
     if live is not None and len(live) != n:
         raise ValueError("live must have one flag per server")
     nlive = n if live is None else int(sum(bool(x) for x in live))
-    cap = 160 * max(nlive, 1) + 16  # sum of floor(pct * 40 * nlive) * 4 <= 160 * nlive
+    cap = (nlive + 10) * 160  # the reference's allocation (KETAMA_CONTINUUM_ADDITION, nc_ketama.c:132-133)
     cont = torch.empty((cap, 2), dtype=torch.int32, device=device)
     lv = None if live is None else (ctypes.c_uint8 * n)(*[1 if x else 0 for x in live])
     cnt = ctypes.c_uint32(0)
@@ -199,7 +226,7 @@ def ketama_build_device(names: Sequence[bytes], weights: Sequence[int], live: Se
 
 
 def server_idx_device(hash_: int | str, dist: int | str, keys, offsets, continuum, nserver: int,
-                      hash_tag: bytes | None = None, out=None, stream=None, shape=None):
+                      hash_tag: bytes | None = None, out=None, stream=None, shape=None, key_end=None):
     """Fused server_pool_idx (src/nc_server.c:647-700) for a device-resident
     batch: hash_tag trimming, the pool's hash, then ketama/modula dispatch over
     `continuum` (continuum_device()). Returns the int32 server index per key."""
@@ -210,6 +237,9 @@ def server_idx_device(hash_: int | str, dist: int | str, keys, offsets, continuu
     n = offsets.numel() - 1
     if hash_tag is not None and len(hash_tag) != 2:
         raise ValueError("hash_tag is two bytes (conf_set_hash_tag)")
+    _check_batch(keys, offsets, key_end)
+    if continuum.dtype != torch.int32 or not continuum.is_cuda or not continuum.is_contiguous():
+        raise ValueError("continuum must be a contiguous int32 CUDA tensor (continuum_device())")
     if out is None:
         out = torch.empty(max(n, 0), dtype=torch.int32, device=keys.device)
     L.check(
@@ -223,6 +253,19 @@ def server_idx_device(hash_: int | str, dist: int | str, keys, offsets, continuu
 
 
 MC_OK, MC_EINVAL, MC_EKEYLEN, MC_EUNSUPPORTED = 0, -1, -2, -3  # NC_GPUHASH_MC_*
+
+
+def _check_stream(stream) -> None:
+    """The parsers read `stream` on the device: it must be a contiguous uint8
+    CUDA tensor (a host tensor's pointer would be dereferenced by a kernel)."""
+    import torch
+
+    if not isinstance(stream, torch.Tensor) or stream.dtype != torch.uint8:
+        raise TypeError("stream must be a uint8 tensor")
+    if not stream.is_cuda:
+        raise ValueError("stream must be a CUDA (HIP) tensor")
+    if not stream.is_contiguous():
+        raise ValueError("stream must be contiguous")
 
 
 class McParser:
@@ -253,6 +296,7 @@ class McParser:
         keys/offsets feed hash_batch_device / server_idx_device directly."""
         import torch
 
+        _check_stream(stream)
         dev = stream.device
         nbytes = stream.numel()
         keys = torch.empty(nbytes + L.NC_GPUHASH_PAD, dtype=torch.uint8, device=dev)
@@ -294,6 +338,7 @@ class RedisParser(McParser):
         """As McParser.parse, with NC_GPUHASH_REDIS_* statuses."""
         import torch
 
+        _check_stream(stream)
         dev = stream.device
         nbytes = stream.numel()
         keys = torch.empty(nbytes + L.NC_GPUHASH_PAD, dtype=torch.uint8, device=dev)
