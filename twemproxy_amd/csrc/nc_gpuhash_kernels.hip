@@ -1661,6 +1661,13 @@ hipError_t entry_dist(const uint8_t *base, const uint64_t *off, uint64_t delta, 
                       hipStream_t stream, const DistArgs &d);
 } // namespace nc_tu
 
+namespace nc_md5 {
+/* md5 on the direct per-lane block pipeline (nc_md5_kernels.hip); keys is any
+ * byte address, nkeys < 2^32 */
+hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
+                  int var);
+} // namespace nc_md5
+
 namespace {
 using nc_tu::g_grid_cap;
 using nc_tu::g_num_cus;
@@ -1677,6 +1684,7 @@ constexpr int kVarRingP4 = 128;
 constexpr int kVarSorted = 1 << 17; /* group the tile's keys by length (the SORT pipeline) */
 constexpr int kVarRingSorted = 128 | 16384; /* 256-key wave tiles hashed in length-sorted rounds (6 KiB slots) */
 constexpr int kVarOver = 1 << 18; /* workgroup pipelines: three resident sets of workgroups per launch */
+constexpr int kVarMd5Direct = 1 << 19; /* md5: the direct per-lane block pipeline (nc_md5_kernels.hip) */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -1989,6 +1997,14 @@ namespace {
  * identical outputs. */
 int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
 {
+    if (mode == NC_GPUHASH_MD5) {
+        /* the direct per-lane block pipeline for every shape; keys of 64+ bytes
+         * on average take its LDS-DMA variant (option bit 2 = variant bit 22),
+         * whose 64-byte pieces spare the texture addresser (C4 shard 3.1 ->
+         * 2.1 ms, 128-byte keys 0.80 -> 0.62 ms; short keys are faster direct) */
+        const bool lds = sh != nullptr && nkeys != 0 && sh->key_bytes / nkeys >= 64u;
+        return kVarMd5Direct | (lds ? (4 << 20) : 0);
+    }
     if (sh == nullptr || nkeys == 0 || sh->key_bytes == 0) return kVarRegStaged;
     const uint64_t mean = sh->key_bytes / nkeys;
     const bool fixed = sh->max_len >= sh->min_len && sh->max_len - sh->min_len <= 4u;
@@ -2031,6 +2047,9 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
     const uint64_t delta = (uint64_t)(kp & 15u);
     const int tuned = load_i(&g_variant);
     int var = tuned != 0 ? tuned : pick_variant(mode, nkeys, shape);
+    if (mode == NC_GPUHASH_MD5 && (var & kVarMd5Direct) != 0 && nkeys < (1ull << 32))
+        return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15); /* bits 20-23: options */
+    var &= ~kVarMd5Direct;
     const bool sort = sort_enabled() || (var & kVarSorted) != 0;
     var &= ~(kVarWorkgroup | kVarSorted); /* kVarOver rides along to launch_kernel */
     /* the wave ring DMAs offsets 16 bytes per lane: it needs 16-byte aligned

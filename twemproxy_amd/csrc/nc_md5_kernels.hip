@@ -1,0 +1,377 @@
+/*
+ * hash_md5 (src/hashkit/nc_md5.c:301-321: md5_signature's digest bytes 0..3 as
+ * a little-endian u32) on gfx950 — the direct per-lane pipeline.
+ *
+ * md5 is VALU-bound (64 steps of ~5 dependent integer ops per 64-byte block),
+ * so this kernel is built around the block, not around the byte stream:
+ *
+ *   - a wave owns a tile of 64 consecutive keys, one per lane, and walks its
+ *     tiles grid-stride (persistent waves, no workgroup barrier anywhere);
+ *   - a ROUND hashes one 64-byte block of every active lane's key. Its
+ *     message words come straight from HBM/L2 with four unaligned 16-byte
+ *     loads per lane (gfx9 global memory runs in unaligned mode), issued one
+ *     round ahead into a second register set, so the loads of round r+1 fly
+ *     while round r computes;
+ *   - the key's last data block is padded in registers by ONE v_perm_b32 per
+ *     word: the selector keeps a message byte, injects the 0x80 pad byte, or
+ *     zeroes it (src/hashkit/nc_md5.c:249-262), and comes from one clamp of a
+ *     per-lane linear form (v_med3_i32) — three VALU ops per word, no
+ *     per-word compares or selects;
+ *   - a key whose padding does not fit its last data block (length % 64 in
+ *     56..63, a multiple of 64, or empty) needs one more block that holds no
+ *     key bytes: 0x80 or 0, zeros, and the bit length (nc_md5.c:263-274).
+ *     Such lanes park their state in a per-wave LDS queue and the wave runs
+ *     those tail blocks 64 at a time, so a Zipf tile with three 60-byte keys
+ *     does not pay a second block for all 64 lanes;
+ *   - the final block of a key stops after step 60: the digest word returned
+ *     is state A (nc_md5.c:317-320), and steps 61-63 only update B, C, D.
+ *
+ * Every round issues the same six vector-memory loads (two offset words,
+ * four message chunks; addresses of chunks a lane does not need are clamped
+ * into the buffer), so hipcc's waitcnt pass can count them exactly.
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <utility>
+
+#include "nc_gpuhash.h"
+#include "nc_hash_algo.h"
+#include "nc_md5_steps.h"
+
+namespace {
+
+using namespace nc_md5s;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+/* ---- message padding by byte permutes ----
+ * Word t of a key's last data block, with m = bytes of the key left in the
+ * block (1..64): bytes j with 4t + j < m are the key's, byte m is 0x80,
+ * the rest are 0. v_perm_b32(d, 0x80000000, sel) picks byte 4+j of d (key
+ * byte j), byte 3 of 0x80000000 (the pad) or bytes 0-2 (zero). The selector
+ * of word t is clamp(Y0 - t * kStep, 0, kKeep):
+ *   kKeep = 0x07060504 (whole word kept), 0 (whole word zero), and for the
+ *   word holding byte m (t = m / 4) one of kBoundary[m % 4], which lies
+ *   strictly between them; kStep exceeds both gaps, so words before t clamp
+ *   to kKeep and words after it to 0. */
+constexpr uint32_t kPadSrc = 0x80000000u;
+constexpr int32_t kKeep = 0x07060504;
+constexpr int32_t kStep = 0x06000000;
+constexpr uint32_t kBoundary0 = 0x02020203u; /* [pad, 0, 0, 0] */
+constexpr uint32_t kBoundary1 = 0x02020304u; /* [key, pad, 0, 0] */
+constexpr uint32_t kBoundary2 = 0x02030504u; /* [key, key, pad, 0] */
+constexpr uint32_t kBoundary3 = 0x03060504u; /* [key, key, key, pad] */
+static_assert(kStep > kKeep - (int32_t)kBoundary0 && kStep > (int32_t)kBoundary3, "selector ordering");
+static_assert(16ll * kStep + (int64_t)kBoundary3 < (1ll << 31), "selector form fits int32");
+
+__device__ __forceinline__ uint32_t pad_word(uint32_t d, int32_t y)
+{
+    const int32_t sel = y < 0 ? 0 : (y > kKeep ? kKeep : y); /* v_med3_i32 */
+    return __builtin_amdgcn_perm(d, kPadSrc, (uint32_t)sel);
+}
+
+/* per-wave LDS queue of keys waiting for their data-free last block */
+constexpr uint32_t kQ = 128;        /* entries per wave (>= 64 + 63) */
+constexpr uint32_t kQWords = 6;     /* A, B, C, D, length, key index */
+constexpr uint32_t kWaves = 4;      /* waves per workgroup */
+constexpr uint32_t kQBytes = kQ * kQWords * 4u;
+constexpr uint32_t kBlkImage = 64u * 64u; /* one 64-byte block of each of a tile's 64 keys */
+
+struct Queue {
+    uint32_t *w; /* SoA: w[f * kQ + slot] */
+    uint32_t head, count; /* wave-uniform */
+};
+
+__device__ __forceinline__ uint32_t lanemask_lt_popc(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+/* Tail blocks of up to 64 queued keys: message 0x80-or-0, zeros, bit length
+ * (src/hashkit/nc_md5.c:263-274); out[index] = A + the block's A. */
+__device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__restrict__ out)
+{
+    const uint32_t n = q.count < 64u ? q.count : 64u;
+    if (lane < n) {
+        const uint32_t slot = (q.head + lane) & (kQ - 1u);
+        const uint32_t st[4] = {q.w[0 * kQ + slot], q.w[1 * kQ + slot], q.w[2 * kQ + slot], q.w[3 * kQ + slot]};
+        const uint32_t len = q.w[4 * kQ + slot], idx = q.w[5 * kQ + slot];
+        uint32_t w[16] = {};
+        w[0] = (len & 63u) == 0u ? 0x80u : 0u;
+        w[14] = len << 3;
+        w[15] = len >> 29;
+        __builtin_nontemporal_store(md5_block_final_a(st, w), out + idx);
+    }
+    q.head = (q.head + n) & (kQ - 1u);
+    q.count -= n;
+}
+
+/* ---- buffer resources (gfx9 raw buffers: DATA_FORMAT 32, no swizzle) ----
+ * Every load and store of the kernel goes through a buffer resource whose
+ * base is wave-uniform (SGPRs) and whose per-lane offset is 32-bit, so the
+ * hot loop does no 64-bit address arithmetic; the resource's size makes loads
+ * past the buffer end return zeros instead of faulting (no clamping). */
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kRsrcWord3 = 0x00020000;
+constexpr int kAuxNt = 2; /* slc: the streaming cache policy (nt) */
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void *base, uint64_t nbytes)
+{
+    const uint32_t n = nbytes > 0xffffffffull ? 0xffffffffu : (uint32_t)nbytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)n, kRsrcWord3);
+}
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+/* A tile's keys as the lanes hold them: key start relative to the tile's
+ * first key (the data resource's base) and length. */
+struct TileKeys {
+    uint64_t s0;   /* wave-uniform: off[k0], the tile's first key */
+    uint32_t srel; /* this lane's key start - s0 */
+    uint32_t len;
+    bool valid;
+};
+
+} // namespace
+
+/*
+ * One wave = one 64-key tile at a time (lane = key). Round (tile, b) hashes
+ * data block b of every key of the tile that has one; its 16 message words
+ * are in `cur`, loaded during the previous round. keys is any byte address;
+ * key i = keys[off[i], off[i+1]); keys stays readable NC_GPUHASH_PAD bytes
+ * past off[nkeys]. A tile of 64 keys spans less than 4 GiB.
+ */
+template <bool LDS>
+__global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__restrict__ keys,
+                                                           const uint64_t *__restrict__ off, uint64_t nkeys,
+                                                           uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
+{
+    __shared__ uint32_t qmem[kWaves * kQWords * kQ];
+    /* LDS: the next round's blocks arrive by LDS-DMA into a per-wave 4 KiB
+     * image (key k's 64 bytes at k * 64) instead of into registers */
+    __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kBlkImage : 16];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    /* a wave owns `chunk` consecutive tiles; the grid covers every tile once
+     * and the hardware dispatcher balances the waves (no persistent grid to
+     * size from an occupancy estimate) */
+    uint64_t tile = ((uint64_t)blockIdx.x * kWaves + wave) * chunk;
+    const uint64_t tlast = ntiles < tile + chunk ? ntiles : tile + chunk;
+    if (tile >= tlast) return;
+    Queue q{qmem + wave * kQWords * kQ, 0u, 0u};
+    const uint64_t kbytes = off[nkeys] + (uint64_t)NC_GPUHASH_PAD; /* readable bytes from keys */
+
+    /* offsets of tile tl (this wave's last tile again past its range, so
+     * every round issues the same loads): the low dwords of each lane's
+     * start and end (a tile spans < 4 GiB), and the 64-bit start of the
+     * tile's first key by a scalar load */
+    struct Offs {
+        uint32_t s, e;
+        uint64_t s0;
+    };
+    auto load_off = [&](uint64_t tl) __attribute__((always_inline)) {
+        const uint64_t k0 = (tl < tlast ? tl : tlast - 1u) * 64u;
+        const rsrc_t r = make_rsrc(off + k0, (nkeys + 1u - k0) * 8u); /* keys past nkeys read 0 */
+        Offs o;
+        o.s = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u), 0, kAuxNt);
+        o.e = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u + 8u), 0, kAuxNt);
+        o.s0 = off[k0];
+        return o;
+    };
+    auto keys_of = [&](uint64_t tl, const Offs &o) __attribute__((always_inline)) {
+        TileKeys t;
+        t.s0 = o.s0;
+        t.srel = o.s - (uint32_t)o.s0;
+        t.len = o.e - o.s;
+        t.valid = tl * 64u + lane < nkeys;
+        return t;
+    };
+    /* block b of the lanes' keys: only the 16-byte chunks that hold key bytes
+     * (a chunk past the key keeps stale words, which the padding masks off);
+     * per-lane unaligned loads cost the texture addresser per active lane, and
+     * it is the bottleneck of short varying keys (C2: 1.6 chunks per key, not 4) */
+    uint8_t *const img = kbuf + (LDS ? wave * kBlkImage : 0u);
+    /* LDS variant: DMA instruction i moves keys 16i .. 16i+15, four lanes per
+     * key (a 64-byte piece each, 16 pieces per instruction instead of 64
+     * scattered lanes: long keys are bound by the texture addresser) */
+    auto dma_blk = [&](const TileKeys &t, uint32_t b) __attribute__((always_inline)) {
+        const rsrc_t r = make_rsrc(keys + t.s0, kbytes - t.s0);
+        const uint32_t j = lane & 3u;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int src = 16 * i + (int)(lane >> 2);
+            const uint32_t vo = (uint32_t)__shfl((int)t.srel, src);
+            const int32_t rem = __shfl((int)t.len, src) - 64 * (int32_t)b;
+            if (rem > (int32_t)(16u * j))
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(img + 1024 * i),
+                                                          16, vo + 64u * b + 16u * j, 0, 0, 0);
+        }
+    };
+    auto load_blk = [&](const TileKeys &t, uint32_t b, u32x4 (&d)[4]) __attribute__((always_inline)) {
+        if constexpr (LDS) {
+            dma_blk(t, b);
+            return;
+        }
+        const rsrc_t r = make_rsrc(keys + t.s0, kbytes - t.s0);
+        const int vo = (int)(t.srel + 64u * b);
+        const int32_t rem = (int32_t)t.len - 64 * (int32_t)b;
+        if (rem > 0) d[0] = __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, 0);
+        if (rem > 16) d[1] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16, 0, 0);
+        if (rem > 32) d[2] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 32, 0, 0);
+        if (rem > 48) d[3] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 48, 0, 0);
+    };
+
+    /* prologue: offsets of the first tile (waited), of the second (in
+     * flight), block 0 of the first tile (in flight) */
+    TileKeys cur_t = keys_of(tile, load_off(tile));
+    Offs no = load_off(tile + 1u);
+    u32x4 d[4];
+    load_blk(cur_t, 0u, d);
+    uint32_t b = 0;
+    uint32_t st[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
+    uint32_t pad_src; /* kPadSrc in a VGPR: a uniform selector takes the perm's SGPR slot */
+    asm volatile("v_mov_b32 %0, %1" : "=v"(pad_src) : "i"(kPadSrc));
+
+    /* One round: block b of every key of the tile that has one. Its message
+     * words are padded out of `d` first; then `d` receives the next round's
+     * loads (block b+1 of this tile if any key has one, else block 0 of the
+     * next tile, whose offsets are in `no`), which fly during the 64 steps. */
+    for (;;) {
+        const bool more = __ballot(cur_t.valid && cur_t.len > 64u * (b + 1u)) != 0ull;
+        const TileKeys nxt_t = keys_of(tile + 1u, no);
+        const int32_t rem = (int32_t)cur_t.len - 64 * (int32_t)b; /* key bytes from this block's start */
+        const uint32_t len = cur_t.len;
+        const bool act = cur_t.valid && rem > 0;
+        uint32_t w[16];
+        if constexpr (LDS) { /* this round's block, DMA'd during the previous round */
+            /* hipcc does not order these reads after the loop-carried LDS-DMA:
+             * wait for every outstanding vector-memory op (the DMA and the
+             * offset loads issued right after it) */
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int c = 0; c < 4; c++) d[c] = *reinterpret_cast<const u32x4 *>(img + lane * 64u + 16u * c);
+        }
+        const u32x4 (&cur)[4] = d;
+        if (act) {
+            const int32_t m = rem < 64 ? rem : 64;
+            const int32_t m0 = __builtin_amdgcn_readfirstlane(m);
+            if (__ballot(m != m0) == 0ull) {
+                /* every active lane ends at the same byte (fixed-length keys):
+                 * the selectors are wave-uniform, computed on the scalar unit */
+                const uint32_t r = (uint32_t)m0 & 3u;
+                const uint32_t bnd = r == 0u ? kBoundary0 : (r == 1u ? kBoundary1 : (r == 2u ? kBoundary2 : kBoundary3));
+                const int32_t y0 = (int32_t)bnd + (m0 >> 2) * kStep;
+#pragma unroll
+                for (int t = 0; t < 16; t++) {
+                    /* the clamp on the scalar unit (hipcc would use v_med3) and
+                     * the selector as the perm's one SGPR operand */
+                    uint32_t sel;
+                    asm("s_max_i32 %0, %1, 0\n\ts_min_i32 %0, %0, %2" : "=&s"(sel) : "s"(y0 - t * kStep), "s"(kKeep));
+                    w[t] = __builtin_amdgcn_perm(cur[t >> 2][t & 3], pad_src, sel);
+                }
+            } else {
+                const uint32_t r = (uint32_t)m & 3u;
+                /* kBoundary[r] without branches: two 64-bit selects and a shift */
+                const uint64_t pair = (r & 2u) ? ((uint64_t)kBoundary3 << 32 | kBoundary2)
+                                               : ((uint64_t)kBoundary1 << 32 | kBoundary0);
+                const uint32_t bnd = (uint32_t)(pair >> (32u * (r & 1u)));
+                const int32_t y0 = (int32_t)bnd + (m >> 2) * kStep;
+#pragma unroll
+                for (int t = 0; t < 16; t++) w[t] = pad_word(cur[t >> 2][t & 3], y0 - t * kStep);
+            }
+            const bool fin = rem <= 55; /* the bit length fits behind the pad */
+            if (fin) {
+                w[14] = len << 3;
+                w[15] = len >> 29;
+            }
+        }
+        if constexpr (LDS) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the image's reads are done */
+        load_blk(more ? cur_t : nxt_t, more ? b + 1u : 0u, d);
+        /* offsets two tiles ahead, straight into `no` (consumed above: a copy
+         * of a register whose load is in flight would make hipcc wait for
+         * every outstanding load, this round's prefetch included); while this
+         * tile still has blocks it re-reads the next tile's words, which
+         * keeps the per-round load count fixed */
+        no = load_off(more ? tile + 1u : tile + 2u);
+        if (act) {
+            const bool fin = rem <= 55;
+            /* steps 0..60 for every lane; a key that ends here is done (A's
+             * last update is step 60), the others run steps 61..63 */
+            uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+            md5_steps(v, w, std::make_integer_sequence<int, 61>{});
+            if (fin) {
+                const rsrc_t rout = make_rsrc(out + tile * 64u, 256u);
+                __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
+            } else {
+                md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
+                st[0] += v[0];
+                st[1] += v[1];
+                st[2] += v[2];
+                st[3] += v[3];
+            }
+        }
+        /* keys whose last data block could not take the length (or empty
+         * keys) queue their state for a data-free tail block */
+        const bool tail = cur_t.valid && ((rem <= 64 && rem >= 56) || (b == 0u && len == 0u));
+        const uint64_t tm = __ballot(tail);
+        if (tm != 0ull) {
+            if (tail) {
+                const uint32_t slot = (q.head + q.count + lanemask_lt_popc(tm)) & (kQ - 1u);
+                q.w[0 * kQ + slot] = st[0];
+                q.w[1 * kQ + slot] = st[1];
+                q.w[2 * kQ + slot] = st[2];
+                q.w[3 * kQ + slot] = st[3];
+                q.w[4 * kQ + slot] = len;
+                q.w[5 * kQ + slot] = (uint32_t)(tile * 64u + lane);
+            }
+            q.count += (uint32_t)__builtin_popcountll(tm);
+            if (q.count >= 64u) run_tail(q, lane, out);
+        }
+
+        /* advance */
+        if (more) {
+            b++;
+        } else {
+            tile++;
+            b = 0;
+            cur_t = nxt_t;
+            st[0] = NC_MD5_A0;
+            st[1] = NC_MD5_B0;
+            st[2] = NC_MD5_C0;
+            st[3] = NC_MD5_D0;
+        }
+        if (tile >= tlast) break;
+    }
+    while (q.count != 0u) run_tail(q, lane, out);
+}
+
+namespace nc_md5 {
+
+/* var: bits 0-1 tiles per wave (0: 16, 1: 8, 2: 32, 3: 64); bit 2: the LDS-DMA
+ * variant (long keys) */
+hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
+                  int var)
+{
+    static const uint32_t kChunk[4] = {16, 8, 32, 64};
+    const uint32_t chunk = kChunk[var & 3];
+    const uint64_t ntiles = (nkeys + 63u) / 64u;
+    const uint64_t grid = (ntiles + (uint64_t)kWaves * chunk - 1u) / ((uint64_t)kWaves * chunk);
+    if (grid > 0x7fffffffu) return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    if (var & 4)
+        hipLaunchKernelGGL(nc_md5_direct_kernel<true>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off, nkeys,
+                           d_out, ntiles, chunk);
+    else
+        hipLaunchKernelGGL(nc_md5_direct_kernel<false>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off,
+                           nkeys, d_out, ntiles, chunk);
+    return hipGetLastError();
+}
+
+} // namespace nc_md5

@@ -1,0 +1,70 @@
+/*
+ * The 64 md5 steps for gfx950 kernels (RFC 1321; src/hashkit/nc_md5.c:89-194),
+ * unrolled at compile time: step I updates one of the four state words
+ * (a, d, c, b in turn). Shared by nc_md5_kernels.hip and the VALU probes.
+ */
+#ifndef NC_MD5_STEPS_H
+#define NC_MD5_STEPS_H
+
+#include <stdint.h>
+
+#include <utility>
+
+#include "nc_hash_algo.h"
+
+namespace nc_md5s {
+
+/* the 64 steps' constants, message word and shift, from NC_MD5_ROUNDS
+ * (RFC 1321; src/hashkit/nc_md5.c:89-194) */
+#define NC_MD5_KT(f, a, b, c, d, k, t, s) t,
+#define NC_MD5_KM(f, a, b, c, d, k, t, s) k,
+#define NC_MD5_KS(f, a, b, c, d, k, t, s) s,
+constexpr uint32_t kT[64] = {NC_MD5_ROUNDS(NC_MD5_KT)};
+constexpr int kM[64] = {NC_MD5_ROUNDS(NC_MD5_KM)};
+constexpr int kS[64] = {NC_MD5_ROUNDS(NC_MD5_KS)};
+
+/* Step I updates one of the four state words: a, d, c, b in turn. */
+template <int I>
+__device__ __forceinline__ void md5_step(uint32_t (&v)[4], const uint32_t (&w)[16])
+{
+    constexpr int u = (4 - (I & 3)) & 3;
+    const uint32_t b = v[(u + 1) & 3], c = v[(u + 2) & 3], d = v[(u + 3) & 3];
+    uint32_t f;
+    if constexpr (I < 16) f = NC_MD5_F(b, c, d);
+    else if constexpr (I < 32) f = NC_MD5_G(b, c, d);
+    else if constexpr (I < 48) f = NC_MD5_H(b, c, d);
+    else f = NC_MD5_I(b, c, d);
+    /* a + w + f by one v_add3_u32, then + T by a VOP2 literal add: five VALU
+     * instructions per step and no scalar s_mov of T (hipcc's default form,
+     * a+w, s_mov T, v_add3, is 5 % slower; three VOP2 adds 15 % slower:
+     * tools/probes/md5_rate.hip) */
+    uint32_t x = v[u] + w[kM[I]] + f;
+    asm("" : "+v"(x)); /* keeps T out of the sum: hipcc would reassociate it into an s_mov + v_add3 */
+    const uint32_t a = x + kT[I];
+    v[u] = nc_rotl(a, kS[I]) + b;
+}
+
+template <int... I>
+__device__ __forceinline__ void md5_steps(uint32_t (&v)[4], const uint32_t (&w)[16], std::integer_sequence<int, I...>)
+{
+    (md5_step<I>(v, w), ...);
+}
+
+template <int... I>
+__device__ __forceinline__ void md5_steps_from61(uint32_t (&v)[4], const uint32_t (&w)[16],
+                                                 std::integer_sequence<int, I...>)
+{
+    (md5_step<61 + I>(v, w), ...);
+}
+
+/* final block: only A is returned, and A's last update is step 60 */
+__device__ __forceinline__ uint32_t md5_block_final_a(const uint32_t (&st)[4], const uint32_t (&w)[16])
+{
+    uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+    md5_steps(v, w, std::make_integer_sequence<int, 61>{});
+    return st[0] + v[0];
+}
+
+} // namespace nc_md5s
+
+#endif
