@@ -1,0 +1,292 @@
+/*
+ * Byte-serial hashkit modes on the direct per-lane pipeline (nc_direct.h):
+ * crc16, crc32, crc32a (src/hashkit/nc_crc16.c:56-66, nc_crc32.c:99-123),
+ * fnv1_64, fnv1a_64, fnv1_32, fnv1a_32 (nc_fnv.c:26-82) and one_at_a_time
+ * (nc_one_at_a_time.c:35-51). One lane hashes one key, 64 bytes per round,
+ * from registers (fixed-length keys: every lane of a wave runs the same byte
+ * count) or, for long keys, from the LDS-DMA block image.
+ *
+ * The crc table lookup is the crc modes' bottleneck on the other pipelines:
+ * one 1 KiB table, a random entry per lane (~3.5-way bank conflicts) and a
+ * dependent lookup per byte. Here whole words go through slicing-by-4 tables
+ * (four independent lookups) replicated over 8 bank groups (see look()).
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "nc_direct.h"
+#include "nc_gpuhash.h"
+#include "nc_hash_algo.h"
+
+namespace {
+
+using namespace nc_direct;
+
+constexpr uint32_t kWaves = 16; /* 1024-thread workgroups share one table */
+
+template <int MODE>
+constexpr bool has_table()
+{
+    return MODE == NC_GPUHASH_CRC16 || MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A;
+}
+
+template <int MODE>
+__device__ __forceinline__ uint32_t init_state()
+{
+    if constexpr (MODE == NC_GPUHASH_FNV1_64 || MODE == NC_GPUHASH_FNV1A_64) return NC_FNV64_INIT32;
+    if constexpr (MODE == NC_GPUHASH_FNV1_32 || MODE == NC_GPUHASH_FNV1A_32) return NC_FNV32_INIT;
+    if constexpr (MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A) return 0xffffffffu;
+    return 0u; /* one_at_a_time, crc16 */
+}
+
+template <int MODE>
+__device__ __forceinline__ uint32_t final_state(uint32_t h)
+{
+    if constexpr (MODE == NC_GPUHASH_ONE_AT_A_TIME) return nc_oaat_final(h);
+    if constexpr (MODE == NC_GPUHASH_CRC32) return nc_crc32_final(h);
+    if constexpr (MODE == NC_GPUHASH_CRC32A) return nc_crc32a_final(h);
+    return h;
+}
+
+/* ---- crc tables: slicing-by-4, replicated over 8 bank groups ----
+ * Four tables T0..T3 of 256 entries: T0 is the byte table
+ * (src/hashkit/nc_crc16.c:20-53, nc_crc32.c:27-92, generated from the
+ * polynomials), Tk advances Tk-1 by one more zero byte, so a whole word costs
+ * four INDEPENDENT lookups (one LDS latency) instead of four chained ones.
+ * Each entry is stored 8 times, copy c for lanes with (lane & 7) == c: lanes
+ * of one copy class meet only when their entries agree mod 4, which keeps a
+ * 64-lane lookup near conflict-free. Word of (table k, entry e, copy c):
+ * (k * 256 + e) * 8 + c. 32 KiB. */
+constexpr uint32_t kCopies = 8;
+constexpr uint32_t kTabWords = 4u * 256u * kCopies;
+
+template <int MODE>
+__device__ __forceinline__ uint32_t tab_entry(uint32_t k, uint32_t e)
+{
+    if constexpr (MODE == NC_GPUHASH_CRC16) { /* Tk[e] = e * x^(16 + 8k) mod P, 16 bits */
+        uint32_t v = nc_crc16_entry(e);
+        for (uint32_t j = 0; j < k; j++) v = ((v << 8) ^ nc_crc16_entry(v >> 8)) & 0xffffu;
+        return v;
+    } else { /* reflected: Tk[e] = (Tk-1[e] >> 8) ^ T0[Tk-1[e] & 0xff] */
+        uint32_t v = nc_crc32_entry(e);
+        for (uint32_t j = 0; j < k; j++) v = (v >> 8) ^ nc_crc32_entry(v & 0xffu);
+        return v;
+    }
+}
+
+/* table k, entry idx (0..255), in this lane's copy: byte address ((k*256 + idx) << 5) | lc4 */
+__device__ __forceinline__ uint32_t look(const uint32_t *tab, uint32_t idx, uint32_t lc4, uint32_t k = 0)
+{
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(tab) + (k << 13) + ((idx << 5) | lc4));
+}
+
+/* byte j (0..3) of word w into state h */
+template <int MODE>
+__device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t w, int j, const uint32_t *tab, uint32_t lane4)
+{
+    const uint32_t b = (w >> (8 * j)) & 0xffu;
+    if constexpr (MODE == NC_GPUHASH_CRC16) return NC_CRC16_NEXT(h, look(tab, NC_CRC16_IDX(h, b), lane4));
+    else if constexpr (MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A)
+        return NC_CRC32_NEXT(h, look(tab, NC_CRC32_IDX(h, b), lane4));
+    else if constexpr (MODE == NC_GPUHASH_FNV1A_64) return nc_fnv1a_64_step(h, b);
+    else if constexpr (MODE == NC_GPUHASH_FNV1_64) return nc_fnv1_64_step(h, b);
+    else if constexpr (MODE == NC_GPUHASH_FNV1_32) return nc_fnv1_32_step(h, b);
+    else if constexpr (MODE == NC_GPUHASH_FNV1A_32) return nc_fnv1a_32_step(h, b);
+    else return nc_oaat_step(h, b);
+}
+
+/* the 4 bytes of word w */
+template <int MODE>
+__device__ __forceinline__ uint32_t word_step(uint32_t h, uint32_t w, const uint32_t *tab, uint32_t lc4)
+{
+    if constexpr (MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A) {
+        /* reflected slicing-by-4: the word meets the state's low bytes */
+        const uint32_t x = h ^ w;
+        return look(tab, x >> 24, lc4, 0) ^ look(tab, (x >> 16) & 0xffu, lc4, 1) ^ look(tab, (x >> 8) & 0xffu, lc4, 2) ^
+               look(tab, x & 0xffu, lc4, 3);
+    } else if constexpr (MODE == NC_GPUHASH_CRC16) {
+        /* MSB-first slicing-by-4 on the 16-bit crc: V = crc << 16 ^ the word's
+         * bytes big-endian; crc' = V * x^16 mod P. The unmasked 32-bit state
+         * (nc_crc16.c:59-65) keeps shifted history in bits 16-31; those are
+         * rebuilt by the byte steps at the key's end (block_step leaves the last
+         * 2+ bytes to them), so here only the low 16 bits are carried. */
+        const uint32_t v = ((h & 0xffffu) << 16) ^ __builtin_bswap32(w);
+        return look(tab, v >> 24, lc4, 3) ^ look(tab, (v >> 16) & 0xffu, lc4, 2) ^ look(tab, (v >> 8) & 0xffu, lc4, 1) ^
+               look(tab, v & 0xffu, lc4, 0);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) h = byte_step<MODE>(h, w, j, tab, lc4);
+        return h;
+    }
+}
+
+/* the first nb (1..4, per lane) bytes of word w, one at a time */
+template <int MODE>
+__device__ __forceinline__ uint32_t bytes_step(uint32_t h, uint32_t w, int32_t nb, const uint32_t *tab, uint32_t lc4)
+{
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (j < nb) h = byte_step<MODE>(h, w, j, tab, lc4);
+    return h;
+}
+
+/* nb (per lane, may exceed 64) key bytes of one block in d */
+template <int MODE>
+__device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], int32_t nb, const uint32_t *tab,
+                                               uint32_t lane4)
+{
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+        const int32_t kb = nb - 4 * t;
+        const uint32_t w = d[t >> 2][t & 3];
+        /* crc16 keeps its key's last 2+ bytes for the byte steps, which
+         * rebuild the state's history bits (see word_step) */
+        constexpr int32_t kWhole = MODE == NC_GPUHASH_CRC16 ? 6 : 4;
+        if (kb >= kWhole) h = word_step<MODE>(h, w, tab, lane4);
+        else if (kb > 0) h = bytes_step<MODE>(h, w, kb, tab, lane4);
+    }
+    return h;
+}
+
+} // namespace
+
+/*
+ * One wave = one 64-key tile at a time (lane = key), `chunk` consecutive
+ * tiles per wave. Round (tile, b) feeds block b (bytes 64b .. 64b+63) of every
+ * key that has one into its state; the next round's block is in flight (the
+ * other register set, or the LDS image) while this one computes.
+ */
+template <int MODE, bool LDS>
+__global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__restrict__ keys,
+                                                              const uint64_t *__restrict__ off, uint64_t nkeys,
+                                                              uint32_t *__restrict__ out, uint64_t ntiles,
+                                                              uint32_t chunk)
+{
+    __shared__ uint32_t tab[has_table<MODE>() ? kTabWords : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kImage : 16];
+    if constexpr (has_table<MODE>()) {
+        for (uint32_t i = threadIdx.x; i < 4u * 256u; i += 1024u) {
+            const uint32_t v = tab_entry<MODE>(i >> 8, i & 255u);
+#pragma unroll
+            for (uint32_t c = 0; c < kCopies; c++) tab[i * kCopies + c] = v;
+        }
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane4 = (lane & (kCopies - 1u)) * 4u; /* this lane's table copy */
+    uint64_t tile = ((uint64_t)blockIdx.x * kWaves + wave) * chunk;
+    const uint64_t tlast = ntiles < tile + chunk ? ntiles : tile + chunk;
+    if (tile >= tlast) return;
+    Walker wk;
+    wk.init(keys, off, nkeys, tlast, lane);
+    uint8_t *const img = kbuf + (LDS ? wave * kImage : 0u);
+
+    TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
+    Offs no = wk.load_off(tile + 1u);
+    u32x4 da[4], db[4];
+    if constexpr (LDS) wk.dma(cur_t, 0u, img);
+    else wk.load_regs(cur_t, 0u, da);
+    uint32_t b = 0;
+    uint32_t h = init_state<MODE>();
+
+    /* one round on `cur`; the next round's block goes to `nxt` (registers) or
+     * to the LDS image */
+    auto round = [&](u32x4 (&cur)[4], u32x4 (&nxt)[4]) __attribute__((always_inline)) {
+        const bool more = __ballot(cur_t.valid && cur_t.len > 64u * (b + 1u)) != 0ull;
+        const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
+        if constexpr (LDS) {
+            wk.read_img(img, cur);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the image's reads are done */
+            wk.dma(more ? cur_t : nxt_t, more ? b + 1u : 0u, img);
+        } else {
+            wk.load_regs(more ? cur_t : nxt_t, more ? b + 1u : 0u, nxt);
+        }
+        /* offsets two tiles ahead, straight into `no` (it was consumed above);
+         * a re-read of the next tile's while this one still has blocks */
+        no = wk.load_off(more ? tile + 1u : tile + 2u);
+
+        const int32_t rem = (int32_t)cur_t.len - 64 * (int32_t)b;
+        if (cur_t.valid && (rem > 0 || (b == 0u && cur_t.len == 0u))) {
+            h = block_step<MODE>(h, cur, rem, tab, lane4);
+            if (rem <= 64) {
+                const rsrc_t rout = make_rsrc(out + tile * 64u, 256u);
+                __builtin_amdgcn_raw_buffer_store_b32(final_state<MODE>(h), rout, (int)(lane * 4u), 0, kAuxNt);
+            }
+        }
+        if (more) {
+            b++;
+        } else {
+            tile++;
+            b = 0;
+            cur_t = nxt_t;
+            h = init_state<MODE>();
+        }
+    };
+    for (;;) {
+        round(da, db);
+        if (tile >= tlast) break;
+        round(db, da);
+        if (tile >= tlast) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
+}
+
+namespace nc_bytes {
+
+template <int MODE>
+hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
+                       hipStream_t stream, int var)
+{
+    static const uint32_t kChunk[4] = {16, 8, 32, 64};
+    const uint32_t chunk = kChunk[var & 3];
+    const uint64_t ntiles = (nkeys + 63u) / 64u;
+    const uint64_t grid = (ntiles + (uint64_t)kWaves * chunk - 1u) / ((uint64_t)kWaves * chunk);
+    if (grid > 0x7fffffffu) return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    if (var & 4)
+        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true>), dim3((unsigned)grid), dim3(1024), 0, stream, d_keys,
+                           d_off, nkeys, d_out, ntiles, chunk);
+    else
+        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false>), dim3((unsigned)grid), dim3(1024), 0, stream, d_keys,
+                           d_off, nkeys, d_out, ntiles, chunk);
+    return hipGetLastError();
+}
+
+/* the byte-serial modes on the direct pipeline; var: bits 0-1 tiles per wave
+ * (16, 8, 32, 64), bit 2 the LDS-DMA block image (long keys). nkeys < 2^32. */
+bool supports(int mode)
+{
+    switch (mode) {
+    case NC_GPUHASH_ONE_AT_A_TIME:
+    case NC_GPUHASH_CRC16:
+    case NC_GPUHASH_CRC32:
+    case NC_GPUHASH_CRC32A:
+    case NC_GPUHASH_FNV1_64:
+    case NC_GPUHASH_FNV1A_64:
+    case NC_GPUHASH_FNV1_32:
+    case NC_GPUHASH_FNV1A_32:
+        return true;
+    default:
+        return false;
+    }
+}
+
+hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
+                  hipStream_t stream, int var)
+{
+    switch (mode) {
+    case NC_GPUHASH_ONE_AT_A_TIME: return launch_mode<NC_GPUHASH_ONE_AT_A_TIME>(d_keys, d_off, nkeys, d_out, stream, var);
+    case NC_GPUHASH_CRC16: return launch_mode<NC_GPUHASH_CRC16>(d_keys, d_off, nkeys, d_out, stream, var);
+    case NC_GPUHASH_CRC32: return launch_mode<NC_GPUHASH_CRC32>(d_keys, d_off, nkeys, d_out, stream, var);
+    case NC_GPUHASH_CRC32A: return launch_mode<NC_GPUHASH_CRC32A>(d_keys, d_off, nkeys, d_out, stream, var);
+    case NC_GPUHASH_FNV1_64: return launch_mode<NC_GPUHASH_FNV1_64>(d_keys, d_off, nkeys, d_out, stream, var);
+    case NC_GPUHASH_FNV1A_64: return launch_mode<NC_GPUHASH_FNV1A_64>(d_keys, d_off, nkeys, d_out, stream, var);
+    case NC_GPUHASH_FNV1_32: return launch_mode<NC_GPUHASH_FNV1_32>(d_keys, d_off, nkeys, d_out, stream, var);
+    case NC_GPUHASH_FNV1A_32: return launch_mode<NC_GPUHASH_FNV1A_32>(d_keys, d_off, nkeys, d_out, stream, var);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+} // namespace nc_bytes

@@ -1,0 +1,143 @@
+/*
+ * The direct per-lane pipeline shared by nc_md5_kernels.hip and
+ * nc_bytes_kernels.hip (gfx950): a wave owns 64-key tiles (lane = key) and
+ * reads each key's bytes in 64-byte blocks, one block of every lane's key per
+ * ROUND, with the next round's block in flight while a round computes.
+ *
+ *   - Every load goes through a buffer resource with a wave-uniform base
+ *     (SGPRs) and a 32-bit per-lane offset: no 64-bit address arithmetic in
+ *     the loop, and loads past the resource end return zeros instead of
+ *     faulting (no clamping).
+ *   - Offsets: each lane loads the low dwords of its key's start and end (a
+ *     64-key tile spans < 4 GiB), the tile's 64-bit base comes by one scalar
+ *     load.
+ *   - A block reaches the lanes either straight into registers (four
+ *     unaligned 16-byte loads per lane, only the chunks that hold key bytes:
+ *     gfx9 global memory runs in unaligned mode), or — for long keys, where
+ *     64 scattered lanes per instruction saturate the texture addresser — by
+ *     LDS-DMA in 64-byte pieces into a per-wave 4 KiB image (key k's block at
+ *     k * 64), 16 pieces per instruction.
+ */
+#ifndef NC_DIRECT_H
+#define NC_DIRECT_H
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "nc_gpuhash.h"
+
+namespace nc_direct {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kRsrcWord3 = 0x00020000; /* gfx9 raw buffer: DATA_FORMAT 32, no swizzle */
+constexpr int kAuxNt = 2;              /* slc: the streaming cache policy (nt) */
+constexpr uint32_t kImage = 64u * 64u; /* one 64-byte block of each of a tile's 64 keys */
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void *base, uint64_t nbytes)
+{
+    const uint32_t n = nbytes > 0xffffffffull ? 0xffffffffu : (uint32_t)nbytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)n, kRsrcWord3);
+}
+
+/* A tile's keys as the lanes hold them. */
+struct TileKeys {
+    uint64_t s0;   /* wave-uniform: off[k0], the tile's first key (the data resource's base) */
+    uint32_t srel; /* this lane's key start - s0 */
+    uint32_t len;
+    bool valid;
+};
+
+/* Offsets of a tile, as loaded (consumed one round later). */
+struct Offs {
+    uint32_t s, e; /* low dwords of this lane's key start and end */
+    uint64_t s0;
+};
+
+struct Walker {
+    const uint8_t *keys;
+    const uint64_t *off;
+    uint64_t nkeys;
+    uint64_t kbytes; /* readable bytes from keys: off[nkeys] + NC_GPUHASH_PAD */
+    uint64_t tlast;  /* end of this wave's tiles */
+    uint32_t lane;
+
+    __device__ __forceinline__ void init(const uint8_t *k, const uint64_t *o, uint64_t n, uint64_t tl, uint32_t ln)
+    {
+        keys = k;
+        off = o;
+        nkeys = n;
+        kbytes = off[n] + (uint64_t)NC_GPUHASH_PAD;
+        tlast = tl;
+        lane = ln;
+    }
+
+    /* offsets of tile tl; this wave's last tile again past its range, so that
+     * every round issues the same loads (keys past nkeys read as 0) */
+    __device__ __forceinline__ Offs load_off(uint64_t tl) const
+    {
+        const uint64_t k0 = (tl < tlast ? tl : tlast - 1u) * 64u;
+        const rsrc_t r = make_rsrc(off + k0, (nkeys + 1u - k0) * 8u);
+        Offs o;
+        o.s = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u), 0, kAuxNt);
+        o.e = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u + 8u), 0, kAuxNt);
+        o.s0 = off[k0];
+        return o;
+    }
+
+    __device__ __forceinline__ TileKeys keys_of(uint64_t tl, const Offs &o) const
+    {
+        TileKeys t;
+        t.s0 = o.s0;
+        t.srel = o.s - (uint32_t)o.s0;
+        t.len = o.e - o.s;
+        t.valid = tl * 64u + lane < nkeys;
+        return t;
+    }
+
+    /* block b of the lanes' keys into registers: only the 16-byte chunks that
+     * hold key bytes (a chunk past the key keeps stale words; callers mask) */
+    __device__ __forceinline__ void load_regs(const TileKeys &t, uint32_t b, u32x4 (&d)[4]) const
+    {
+        const rsrc_t r = make_rsrc(keys + t.s0, kbytes - t.s0);
+        const int vo = (int)(t.srel + 64u * b);
+        const int32_t rem = (int32_t)t.len - 64 * (int32_t)b;
+        if (rem > 0) d[0] = __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, 0);
+        if (rem > 16) d[1] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16, 0, 0);
+        if (rem > 32) d[2] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 32, 0, 0);
+        if (rem > 48) d[3] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 48, 0, 0);
+    }
+
+    /* block b of the lanes' keys into the wave's LDS image by LDS-DMA:
+     * instruction i moves keys 16i .. 16i+15, four lanes per key */
+    __device__ __forceinline__ void dma(const TileKeys &t, uint32_t b, uint8_t *img) const
+    {
+        const rsrc_t r = make_rsrc(keys + t.s0, kbytes - t.s0);
+        const uint32_t j = lane & 3u;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int src = 16 * i + (int)(lane >> 2);
+            const uint32_t vo = (uint32_t)__shfl((int)t.srel, src);
+            const int32_t rem = __shfl((int)t.len, src) - 64 * (int32_t)b;
+            if (rem > (int32_t)(16u * j))
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(img + 1024 * i),
+                                                          16, vo + 64u * b + 16u * j, 0, 0, 0);
+        }
+    }
+
+    /* this lane's block from the LDS image, DMA'd during the previous round.
+     * hipcc does not order these reads after a loop-carried LDS-DMA: wait for
+     * every outstanding vector-memory op (the DMA and the offset loads issued
+     * right after it) */
+    __device__ __forceinline__ void read_img(const uint8_t *img, u32x4 (&d)[4]) const
+    {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < 4; c++) d[c] = *reinterpret_cast<const u32x4 *>(img + lane * 64u + 16u * c);
+    }
+};
+
+} // namespace nc_direct
+
+#endif

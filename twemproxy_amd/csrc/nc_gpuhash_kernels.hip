@@ -1668,6 +1668,13 @@ hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, 
                   int var);
 } // namespace nc_md5
 
+namespace nc_bytes {
+/* the byte-serial modes on the direct pipeline (nc_bytes_kernels.hip) */
+bool supports(int mode);
+hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
+                  hipStream_t stream, int var);
+} // namespace nc_bytes
+
 namespace {
 using nc_tu::g_grid_cap;
 using nc_tu::g_num_cus;
@@ -1684,7 +1691,10 @@ constexpr int kVarRingP4 = 128;
 constexpr int kVarSorted = 1 << 17; /* group the tile's keys by length (the SORT pipeline) */
 constexpr int kVarRingSorted = 128 | 16384; /* 256-key wave tiles hashed in length-sorted rounds (6 KiB slots) */
 constexpr int kVarOver = 1 << 18; /* workgroup pipelines: three resident sets of workgroups per launch */
-constexpr int kVarMd5Direct = 1 << 19; /* md5: the direct per-lane block pipeline (nc_md5_kernels.hip) */
+constexpr int kVarMd5Direct = 1 << 19; /* the direct per-lane block pipeline: md5 (nc_md5_kernels.hip) and
+                                          the byte-serial modes (nc_bytes_kernels.hip); options in bits 20-23 */
+constexpr int kVarDirect = kVarMd5Direct;
+constexpr int kVarDirectLds = 4 << 20; /* its LDS-DMA block image (long keys) */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2012,11 +2022,22 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
     const bool fnv_like = mode == NC_GPUHASH_FNV1_64 || mode == NC_GPUHASH_FNV1A_64 || mode == NC_GPUHASH_FNV1_32 ||
                           mode == NC_GPUHASH_FNV1A_32 || mode == NC_GPUHASH_HSIEH || mode == NC_GPUHASH_MURMUR;
     const bool md5 = mode == NC_GPUHASH_MD5;
-    if (mean >= 80u) { /* tiles overflow the workgroup slab: wave ring, deeper or wider slab slots */
-        if (md5) return mean >= 192u ? kVarRingP5 : (kVarWorkgroup | kVarOver);
-        if (mode == NC_GPUHASH_ONE_AT_A_TIME || mode == NC_GPUHASH_HSIEH) return kVarRingP5;
+    /* the byte-serial modes of the direct pipeline (nc_bytes_kernels.hip) */
+    const bool direct_bytes = crc || mode == NC_GPUHASH_ONE_AT_A_TIME || mode == NC_GPUHASH_FNV1_64 ||
+                              mode == NC_GPUHASH_FNV1A_64 || mode == NC_GPUHASH_FNV1_32 || mode == NC_GPUHASH_FNV1A_32;
+    if (mean >= 80u) {
+        /* long keys: the direct pipeline's LDS-DMA block image (C4 shard
+         * crc32 3.56 -> 2.24 ms, fnv1a_64 3.06 -> 2.15, one_at_a_time 3.22 ->
+         * 2.48; 128-byte keys 0.79 -> 0.62 ms); the word modes keep the wave
+         * ring, deeper or wider slab slots */
+        if (direct_bytes) return kVarDirect | kVarDirectLds;
+        if (mode == NC_GPUHASH_HSIEH) return kVarRingP5;
         return kVarRingP4;
     }
+    /* fixed-length short keys: the crcs' slicing-by-4 tables on the direct
+     * pipeline (C3: 0.70 -> 0.61 ms); varying lengths keep the length-grouped
+     * workgroup pipelines (a direct wave runs to its longest key) */
+    if (crc && fixed && mean <= 64u) return kVarDirect;
     if (fixed) {
         if (mean >= 20u && mean <= 40u) { /* C3 */
             if (fnv_like) return kVarRingP5;
@@ -2047,9 +2068,11 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
     const uint64_t delta = (uint64_t)(kp & 15u);
     const int tuned = load_i(&g_variant);
     int var = tuned != 0 ? tuned : pick_variant(mode, nkeys, shape);
-    if (mode == NC_GPUHASH_MD5 && (var & kVarMd5Direct) != 0 && nkeys < (1ull << 32))
-        return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15); /* bits 20-23: options */
-    var &= ~kVarMd5Direct;
+    if ((var & kVarDirect) != 0 && nkeys < (1ull << 32)) { /* bits 20-23: options */
+        if (mode == NC_GPUHASH_MD5) return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
+        if (nc_bytes::supports(mode)) return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
+    }
+    var &= ~(kVarDirect | (15 << 20));
     const bool sort = sort_enabled() || (var & kVarSorted) != 0;
     var &= ~(kVarWorkgroup | kVarSorted); /* kVarOver rides along to launch_kernel */
     /* the wave ring DMAs offsets 16 bytes per lane: it needs 16-byte aligned

@@ -39,12 +39,13 @@
 #include "nc_gpuhash.h"
 #include "nc_hash_algo.h"
 #include "nc_md5_steps.h"
+#include "nc_direct.h"
 
 namespace {
 
 using namespace nc_md5s;
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+using namespace nc_direct;
 
 /* ---- message padding by byte permutes ----
  * Word t of a key's last data block, with m = bytes of the key left in the
@@ -77,7 +78,6 @@ constexpr uint32_t kQ = 128;        /* entries per wave (>= 64 + 63) */
 constexpr uint32_t kQWords = 6;     /* A, B, C, D, length, key index */
 constexpr uint32_t kWaves = 4;      /* waves per workgroup */
 constexpr uint32_t kQBytes = kQ * kQWords * 4u;
-constexpr uint32_t kBlkImage = 64u * 64u; /* one 64-byte block of each of a tile's 64 keys */
 
 struct Queue {
     uint32_t *w; /* SoA: w[f * kQ + slot] */
@@ -108,37 +108,6 @@ __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__re
     q.count -= n;
 }
 
-/* ---- buffer resources (gfx9 raw buffers: DATA_FORMAT 32, no swizzle) ----
- * Every load and store of the kernel goes through a buffer resource whose
- * base is wave-uniform (SGPRs) and whose per-lane offset is 32-bit, so the
- * hot loop does no 64-bit address arithmetic; the resource's size makes loads
- * past the buffer end return zeros instead of faulting (no clamping). */
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-constexpr int kRsrcWord3 = 0x00020000;
-constexpr int kAuxNt = 2; /* slc: the streaming cache policy (nt) */
-
-__device__ __forceinline__ rsrc_t make_rsrc(const void *base, uint64_t nbytes)
-{
-    const uint32_t n = nbytes > 0xffffffffull ? 0xffffffffu : (uint32_t)nbytes;
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)n, kRsrcWord3);
-}
-
-__device__ __forceinline__ uint64_t uniform64(uint64_t v)
-{
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
-
-/* A tile's keys as the lanes hold them: key start relative to the tile's
- * first key (the data resource's base) and length. */
-struct TileKeys {
-    uint64_t s0;   /* wave-uniform: off[k0], the tile's first key */
-    uint32_t srel; /* this lane's key start - s0 */
-    uint32_t len;
-    bool valid;
-};
-
 } // namespace
 
 /*
@@ -156,7 +125,7 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
     __shared__ uint32_t qmem[kWaves * kQWords * kQ];
     /* LDS: the next round's blocks arrive by LDS-DMA into a per-wave 4 KiB
      * image (key k's 64 bytes at k * 64) instead of into registers */
-    __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kBlkImage : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kImage : 16];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     /* a wave owns `chunk` consecutive tiles; the grid covers every tile once
@@ -166,72 +135,18 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
     const uint64_t tlast = ntiles < tile + chunk ? ntiles : tile + chunk;
     if (tile >= tlast) return;
     Queue q{qmem + wave * kQWords * kQ, 0u, 0u};
-    const uint64_t kbytes = off[nkeys] + (uint64_t)NC_GPUHASH_PAD; /* readable bytes from keys */
-
-    /* offsets of tile tl (this wave's last tile again past its range, so
-     * every round issues the same loads): the low dwords of each lane's
-     * start and end (a tile spans < 4 GiB), and the 64-bit start of the
-     * tile's first key by a scalar load */
-    struct Offs {
-        uint32_t s, e;
-        uint64_t s0;
-    };
-    auto load_off = [&](uint64_t tl) __attribute__((always_inline)) {
-        const uint64_t k0 = (tl < tlast ? tl : tlast - 1u) * 64u;
-        const rsrc_t r = make_rsrc(off + k0, (nkeys + 1u - k0) * 8u); /* keys past nkeys read 0 */
-        Offs o;
-        o.s = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u), 0, kAuxNt);
-        o.e = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u + 8u), 0, kAuxNt);
-        o.s0 = off[k0];
-        return o;
-    };
-    auto keys_of = [&](uint64_t tl, const Offs &o) __attribute__((always_inline)) {
-        TileKeys t;
-        t.s0 = o.s0;
-        t.srel = o.s - (uint32_t)o.s0;
-        t.len = o.e - o.s;
-        t.valid = tl * 64u + lane < nkeys;
-        return t;
-    };
-    /* block b of the lanes' keys: only the 16-byte chunks that hold key bytes
-     * (a chunk past the key keeps stale words, which the padding masks off);
-     * per-lane unaligned loads cost the texture addresser per active lane, and
-     * it is the bottleneck of short varying keys (C2: 1.6 chunks per key, not 4) */
-    uint8_t *const img = kbuf + (LDS ? wave * kBlkImage : 0u);
-    /* LDS variant: DMA instruction i moves keys 16i .. 16i+15, four lanes per
-     * key (a 64-byte piece each, 16 pieces per instruction instead of 64
-     * scattered lanes: long keys are bound by the texture addresser) */
-    auto dma_blk = [&](const TileKeys &t, uint32_t b) __attribute__((always_inline)) {
-        const rsrc_t r = make_rsrc(keys + t.s0, kbytes - t.s0);
-        const uint32_t j = lane & 3u;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int src = 16 * i + (int)(lane >> 2);
-            const uint32_t vo = (uint32_t)__shfl((int)t.srel, src);
-            const int32_t rem = __shfl((int)t.len, src) - 64 * (int32_t)b;
-            if (rem > (int32_t)(16u * j))
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(img + 1024 * i),
-                                                          16, vo + 64u * b + 16u * j, 0, 0, 0);
-        }
-    };
+    Walker wk;
+    wk.init(keys, off, nkeys, tlast, lane);
+    uint8_t *const img = kbuf + (LDS ? wave * kImage : 0u);
     auto load_blk = [&](const TileKeys &t, uint32_t b, u32x4 (&d)[4]) __attribute__((always_inline)) {
-        if constexpr (LDS) {
-            dma_blk(t, b);
-            return;
-        }
-        const rsrc_t r = make_rsrc(keys + t.s0, kbytes - t.s0);
-        const int vo = (int)(t.srel + 64u * b);
-        const int32_t rem = (int32_t)t.len - 64 * (int32_t)b;
-        if (rem > 0) d[0] = __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, 0);
-        if (rem > 16) d[1] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16, 0, 0);
-        if (rem > 32) d[2] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 32, 0, 0);
-        if (rem > 48) d[3] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 48, 0, 0);
+        if constexpr (LDS) wk.dma(t, b, img);
+        else wk.load_regs(t, b, d);
     };
 
     /* prologue: offsets of the first tile (waited), of the second (in
      * flight), block 0 of the first tile (in flight) */
-    TileKeys cur_t = keys_of(tile, load_off(tile));
-    Offs no = load_off(tile + 1u);
+    TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
+    Offs no = wk.load_off(tile + 1u);
     u32x4 d[4];
     load_blk(cur_t, 0u, d);
     uint32_t b = 0;
@@ -245,19 +160,12 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
      * next tile, whose offsets are in `no`), which fly during the 64 steps. */
     for (;;) {
         const bool more = __ballot(cur_t.valid && cur_t.len > 64u * (b + 1u)) != 0ull;
-        const TileKeys nxt_t = keys_of(tile + 1u, no);
+        const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
         const int32_t rem = (int32_t)cur_t.len - 64 * (int32_t)b; /* key bytes from this block's start */
         const uint32_t len = cur_t.len;
         const bool act = cur_t.valid && rem > 0;
         uint32_t w[16];
-        if constexpr (LDS) { /* this round's block, DMA'd during the previous round */
-            /* hipcc does not order these reads after the loop-carried LDS-DMA:
-             * wait for every outstanding vector-memory op (the DMA and the
-             * offset loads issued right after it) */
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int c = 0; c < 4; c++) d[c] = *reinterpret_cast<const u32x4 *>(img + lane * 64u + 16u * c);
-        }
+        if constexpr (LDS) wk.read_img(img, d); /* this round's block, DMA'd during the previous round */
         const u32x4 (&cur)[4] = d;
         if (act) {
             const int32_t m = rem < 64 ? rem : 64;
@@ -299,7 +207,7 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
          * every outstanding load, this round's prefetch included); while this
          * tile still has blocks it re-reads the next tile's words, which
          * keeps the per-round load count fixed */
-        no = load_off(more ? tile + 1u : tile + 2u);
+        no = wk.load_off(more ? tile + 1u : tile + 2u);
         if (act) {
             const bool fin = rem <= 55;
             /* steps 0..60 for every lane; a key that ends here is done (A's
