@@ -4,25 +4,36 @@
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N ... bench.py --gpus N ...   (one rank per GPU, RCCL)
 
-Workload (BASELINE.json configs[1]): fnv1a_64 over 2^26 keys
-per GPU with Zipf lengths 8-64 B (s = 1.0), synthetic bytes 0x00-0xFF,
+Headline (BASELINE.json configs[1]): fnv1a_64 over 2^26
+keys per GPU with Zipf lengths 8-64 B (s = 1.0), synthetic bytes 0x00-0xFF,
 device-resident. A step = one kernel pass over one rank's batch. For N > 1
 rank 0 generates all N x 2^26 keys and scatters byte-balanced ranges over
 RCCL (grouped point-to-point); scatter time is reported separately and is
 not part of `value` (weak scaling: fixed keys per GPU).
 
 Rank 0 prints ONE JSON line. `value` = total keys hashed by all ranks per
-second (Mkeys/s) over K timed steps, max over ranks. Extra fields: the md5
-rate on the same keys, the C3 shape (2^26 x 32 B, fnv1a_64) the north-star
-70 % roofline target is quoted on, the HBM roofline of the dominant kernel
-(HIP events on the launch stream), and the reference CPU hashkit timed on
-this host (rank 0, N = 1).
+second (Mkeys/s) over K timed steps, max over ranks. Beside it, each timed
+with HIP events on the launch stream:
+  md5         the same C2 keys (the metric's second mode), against the VALU
+              issue ceiling as well as HBM;
+  c3_*        2^26 x 32 B keys (configs[2]; the north-star 70 % target is
+              quoted on fnv1a_64 here), crc32 with its LDS traffic, md5;
+  c4_shard    one GPU's share of configs[3]: 2^25 x 256 B keys, md5, crc32
+              and fnv1a_64; for N > 1 rank 0 generates all N shards and
+              scatters them over RCCL first (configs[3]'s root scatter);
+  server_idx  fused hash -> ketama dispatch on the C2 keys (§8f.1);
+  redis_key_extraction  2^20 pipelined RESP GETs parsed on the device (§8f.4);
+  c5_e2e      the pipelined GET replay (configs[4]) through the host batch
+              API, PCIe-inclusive (tools/nc_c5_replay);
+  cpu_baseline  the reference hashkit compiled from /root/reference, timed on
+              this host (rank 0, N = 1).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -32,6 +43,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
+VALU_PEAK = 78.6432e12  # lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (one wave64 op per 2 cycles)
+LDS_PEAK_GBS = 78643.2  # ds_read_b32: 128 B/clk/CU x 256 CUs x 2.4 GHz (MI355X_MICROARCH.md LDS table)
+MD5_OPS_PER_BLOCK = 324  # 64 steps x 5 VALU ops (F, 2 adds, rotate, add) + 4 state adds
 SPINUP_S = 0.5  # untimed launches before the warm-up steps (clock ramp)
 METRIC = "Mkeys/s + GB/s hashed (device-resident), fnv1a_64 & md5, 1/2/4/8 MI355X"
 
@@ -45,21 +59,23 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--nkeys", type=int, default=1 << 26, help="keys per GPU")
+    p.add_argument("--nkeys", type=int, default=1 << 26, help="C2 keys per GPU")
+    p.add_argument("--c4-nkeys", type=int, default=1 << 25, help="C4 keys per GPU (256 B each)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    p.add_argument("--no-extra", action="store_true", help="skip md5 / C3 secondary measurements")
+    p.add_argument("--no-extra", action="store_true", help="skip every secondary leg")
+    p.add_argument("--no-c4", action="store_true", help="skip the C4 shard leg")
     p.add_argument("--cpu-sample", type=int, default=1 << 24, help="keys in the CPU baseline sample")
     return p.parse_args()
 
 
-def timed_steps(t, torch, mode, keys, off, out, steps, warmup, dist_on, shape=None, launch=None):
+def timed_steps(t, torch, mode, keys, off, out, steps, warmup, dist_on, shape=None, launch=None, key_end=None):
     """W untimed + K timed launches; wall time bracketed by barrier+sync,
     kernel time by HIP events recorded on the launch stream. `shape` is what
     the packer knows (key bytes, min/max length): it picks the pipeline.
     `launch(stream)` replaces the hash launch (the fused dispatch leg)."""
     if launch is None:
         def launch(stream=None):
-            t.hash_batch_device(mode, keys, off, out, stream=stream, shape=shape)
+            t.hash_batch_device(mode, keys, off, out, stream=stream, shape=shape, key_end=key_end)
     # device clocks ramp up under load: the first ~20 launches of a cold GPU
     # run 5-50 % slow (tools/timing_check.py), so spin for SPINUP_S untimed
     # before the W warm-up steps
@@ -124,6 +140,47 @@ def roofline(alg_bytes: float, kern_ms: float, traffic):
         r["traffic_source"] = traffic["source"]
         r["traffic_over_alg"] = round(traffic["bytes_per_launch"] / alg_bytes, 4)
     return r
+
+
+def md5_ops(torch, off) -> float:
+    """algorithmic VALU lane-ops of md5 over a batch: 324 per 64-byte block,
+    floor((len + 8) / 64) + 1 blocks per key (the padding and the 64-bit
+    length, src/hashkit/nc_md5.c:249-274)."""
+    lens = off[1:] - off[:-1]
+    return float(((lens + 8) // 64 + 1).sum().item()) * MD5_OPS_PER_BLOCK
+
+
+def valu_roofline(ops: float, kern_ms: float, ceiling):
+    achieved = ops / (kern_ms * 1e-3)
+    r = {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(VALU_PEAK / 1e12, 3),
+         "unit": "Tlane-op/s", "frac": round(achieved / VALU_PEAK, 4), "alg_ops_per_launch": int(ops),
+         "ops_per_block": MD5_OPS_PER_BLOCK}
+    if ceiling:
+        r["md5_compute_ceiling"] = ceiling
+        r["frac_of_md5_compute_ceiling"] = round(achieved / (ceiling["tlane_ops_s"] * 1e12), 4)
+    return r
+
+
+def md5_ceiling():
+    """Compute-only md5 rate on this GPU (tools/probes/md5_rate: the kernel's
+    61-step block on register-resident words, no memory traffic): the ceiling
+    the VALU fraction is read against — md5's steps are half VOP3 ops, which
+    issue at half the rate the nominal peak assumes."""
+    exe = os.path.join(HERE, "tools", "probes", "md5_rate")
+    if not os.path.exists(exe):
+        return None
+    try:
+        out = subprocess.run([exe], capture_output=True, text=True, timeout=60, check=True).stdout
+    except Exception:
+        return None
+    rows = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    best = min((r for r in rows if r.get("form") == 2), key=lambda r: r["ns_per_round_per_simd"], default=None)
+    if best is None:
+        return None
+    # one round = 64 lanes x one 61-step final block (61 x 5 ops + 1 add)
+    ops = 64 * (61 * 5 + 1)
+    return {"tlane_ops_s": round(ops * 1024 / (best["ns_per_round_per_simd"] * 1e-9) / 1e12, 3),
+            "source": "tools/probes/md5_rate.hip (form 2, 8 waves/SIMD)"}
 
 
 def read_ceiling(t, rf, buf):
@@ -206,6 +263,19 @@ def cpu_baseline(t, spec, n, mode_names, reps=5):
             "threads_share": share, "cpu_model": cpu_model, "detail": res}
 
 
+def leg(t, torch, mode, keys, off, out, steps, warmup, dist_on, shape, key_end, nk, kb, workload, traffic_key):
+    """one timed mode on one resident batch: value (all ranks), kernel ms, HBM roofline"""
+    w, k = timed_steps(t, torch, mode, keys, off, out, steps, warmup, dist_on, shape, key_end=key_end)
+    w = max_over_ranks(torch, w, dist_on)
+    kmax = max_over_ranks(torch, k, dist_on)
+    return {"workload": workload, "value": round(sum_over_ranks(torch, float(nk), dist_on) * steps / w / 1e6, 1),
+            "unit": "Mkeys/s",
+            "gb_per_s_hashed": round(sum_over_ranks(torch, float(kb), dist_on) * steps / w / 1e9, 2),
+            "kernel_ms": round(k, 4), "kernel_ms_max": round(kmax, 4), "steps": steps,
+            "variant": t.pick_variant(mode, nk, shape),
+            "roofline": roofline(kb + 12.0 * nk, k, load_traffic(mode, traffic_key))}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,36 +295,40 @@ def main():
     spec = t.CONFIGS["C2"]["spec"]
     n_local = args.nkeys
     dev = torch.device("cuda", local)
+    ceiling = md5_ceiling() if (rank == 0 and not args.no_extra) else None
 
-    # ---- input: device-resident before the timed region
-    scatter = None
-    if dist_on:
+    def resident(spec_, n_per_rank):
+        """a config's keys on every rank before any timed region: generated
+        locally at N = 1; at N > 1 generated on rank 0 and scattered"""
+        if not dist_on:
+            k_, o_ = t.synth_device(spec_, 0, n_per_rank, device=dev)
+            return k_, o_, 0, None
         import torch.distributed as dist
 
-        full_k = full_o = None
+        fk = fo = None
         if rank == 0:
-            full_k, full_o = t.synth_device(spec, 0, n_local * world, device=dev)
+            fk, fo = t.synth_device(spec_, 0, n_per_rank * world, device=dev)
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        keys, off, first = scatter_shards(full_k, full_o, dev)
+        k_, o_, first_ = scatter_shards(fk, fo, dev)
         torch.cuda.synchronize()
         dist.barrier()
-        sc_s = time.perf_counter() - t0
-        moved = int(full_k.numel() + full_o.numel() * 8) if rank == 0 else 0
-        del full_k, full_o
+        sc = {"ms": round((time.perf_counter() - t0) * 1e3, 2),
+              "root_egress_bytes": int(fk.numel() + fo.numel() * 8) if rank == 0 else 0,
+              "how": "rank 0 -> every rank, one grouped batch_isend_irecv (RCCL point-to-point over xGMI)"}
+        del fk, fo
         torch.cuda.empty_cache()
-        scatter = {"ms": round(sc_s * 1e3, 2), "root_egress_bytes": moved}
-    else:
-        keys, off = t.synth_device(spec, 0, n_local, device=dev)
-        first = 0
+        return k_, o_, first_, sc
+
+    # ---- headline: fnv1a_64 on C2
+    keys, off, first, scatter = resident(spec, n_local)
     nk = off.numel() - 1
     key_bytes = int(off[-1].item())
     out = torch.empty(nk, dtype=torch.int32, device=dev)
-
-    # ---- headline: fnv1a_64
     shape = spec.shape(key_bytes)
-    wall, kern_ms = timed_steps(t, torch, "fnv1a_64", keys, off, out, args.steps, args.warmup, dist_on, shape)
+    wall, kern_ms = timed_steps(t, torch, "fnv1a_64", keys, off, out, args.steps, args.warmup, dist_on, shape,
+                                key_end=key_bytes)
     wall = max_over_ranks(torch, wall, dist_on)
     kern_ms_max = max_over_ranks(torch, kern_ms, dist_on)
     total_keys = sum_over_ranks(torch, float(nk), dist_on) * args.steps
@@ -268,57 +342,97 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "Mkeys/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (splitmix64 counter generator, SURVEY.md §8d seed 2)",
+        "data": "synthetic (splitmix64 counter generator, SURVEY.md §8d seeds 2-5)",
         "config": {"workload": f"C2: fnv1a_64 over {n_local} keys per GPU, Zipf lengths 8-64 B (s=1.0, "
                                "mean ~19.3 B), bytes 0x00-0xFF, device-resident",
                    "hash": "fnv1a_64", "nkeys_per_gpu": n_local, "key_bytes_rank0": key_bytes,
                    "parallelism": f"shard{world}" if world > 1 else "single"},
         "gb_per_s_hashed": round(total_bytes / wall / 1e9, 2),
         "kernel_ms_rank0": round(kern_ms, 4), "kernel_ms_max": round(kern_ms_max, 4),
+        "variant": t.pick_variant("fnv1a_64", nk, shape),
         "roofline": rf,
     }
     if scatter:
         res["scatter"] = scatter
 
-    # ---- md5 on the same keys; C3 shape for the 70 % target
     if not args.no_extra:
-        w5, k5 = timed_steps(t, torch, "md5", keys, off, out, max(3, args.steps // 4), 1, dist_on, shape)
-        w5 = max_over_ranks(torch, w5, dist_on)
-        s5 = max(3, args.steps // 4)
-        res["md5"] = {"value": round(sum_over_ranks(torch, float(nk), dist_on) * s5 / w5 / 1e6, 1),
-                      "unit": "Mkeys/s", "gb_per_s_hashed": round(sum_over_ranks(torch, float(key_bytes), dist_on) * s5 / w5 / 1e9, 2),
-                      "roofline": roofline(alg, k5, load_traffic("md5", "C2"))}
-        # fused server_pool_idx: fnv1a_64 + ketama_dispatch over
+        # ---- md5 on the same keys: HBM and VALU rooflines
+        s5 = max(5, args.steps // 2)
+        m = leg(t, torch, "md5", keys, off, out, s5, 1, dist_on, shape, key_bytes, nk, key_bytes,
+                "C2 keys, md5", "C2")
+        m["roofline_hbm"] = m.pop("roofline")
+        m["roofline"] = valu_roofline(md5_ops(torch, off), m["kernel_ms"], ceiling)  # md5's binding ceiling
+        res["md5"] = m
+        # ---- fused server_pool_idx: fnv1a_64 + ketama_dispatch over
         # a synthetic sorted continuum of 8 servers x 160 points (LDS-staged)
         rng = np.random.default_rng(9)
         cvals = np.sort(rng.integers(0, 1 << 32, size=8 * 160, dtype=np.uint64)).astype(np.uint32)
         cidx = rng.integers(0, 8, size=cvals.size).astype(np.uint32)
         cont = t.continuum_device(cidx, cvals, device=dev)
-        sidx = max(3, args.steps // 4)
+        sidx = max(5, args.steps // 2)
         wd, kdd = timed_steps(t, torch, None, None, None, None, sidx, 1, dist_on, launch=lambda stream=None:
                               t.server_idx_device("fnv1a_64", "ketama", keys, off, cont, 8, out=out, stream=stream,
-                                                                shape=shape))
+                                                  shape=shape, key_end=key_bytes))
         wd = max_over_ranks(torch, wd, dist_on)
         res["server_idx_ketama"] = {
             "workload": "C2 keys, fnv1a_64 + ketama_dispatch, 8 servers x 160 points (LDS-staged continuum)",
             "value": round(sum_over_ranks(torch, float(nk), dist_on) * sidx / wd / 1e6, 1), "unit": "Mkeys/s",
-            "kernel_ms": round(kdd, 4), "roofline": roofline(alg, kdd, None)}
-        del keys, off, out
-        torch.cuda.empty_cache()
+            "kernel_ms": round(kdd, 4), "roofline": roofline(alg, kdd, load_traffic("server_idx", "C2"))}
+    del keys, off, out
+    torch.cuda.empty_cache()
+
+    if not args.no_extra:
+        # ---- C3 shape: fnv1a_64 (the 70 % target), crc32 (+ its LDS traffic), md5
         c3 = t.CONFIGS["C3"]["spec"]
-        keys3, off3 = t.synth_device(c3, first, n_local, device=dev)
-        out3 = torch.empty(n_local, dtype=torch.int32, device=dev)
+        keys3, off3, _, sc3 = resident(c3, n_local)
+        nk3 = off3.numel() - 1
         kb3 = int(off3[-1].item())
-        w3, k3 = timed_steps(t, torch, "fnv1a_64", keys3, off3, out3, args.steps, args.warmup, dist_on,
-                             c3.shape(kb3))
-        w3 = max_over_ranks(torch, w3, dist_on)
-        res["c3_fnv1a_64"] = {
-            "workload": f"C3 shape: fnv1a_64 over {n_local} x 32 B keys per GPU",
-            "value": round(sum_over_ranks(torch, float(n_local), dist_on) * args.steps / w3 / 1e6, 1),
-            "unit": "Mkeys/s", "kernel_ms": round(k3, 4),
-            "roofline": roofline(kb3 + 12.0 * n_local, k3, load_traffic("fnv1a_64", "C3"))}
-        read_ceiling(t, res["c3_fnv1a_64"]["roofline"], keys3)
+        out3 = torch.empty(nk3, dtype=torch.int32, device=dev)
+        sh3 = c3.shape(kb3)
+        f3 = leg(t, torch, "fnv1a_64", keys3, off3, out3, args.steps, args.warmup, dist_on, sh3, kb3, nk3, kb3,
+                 f"C3: fnv1a_64 over {n_local} x 32 B keys per GPU", "C3")
+        read_ceiling(t, f3["roofline"], keys3)
+        res["c3_fnv1a_64"] = f3
+        c = leg(t, torch, "crc32", keys3, off3, out3, args.steps, args.warmup, dist_on, sh3, kb3, nk3, kb3,
+                f"C3: crc32 over {n_local} x 32 B keys per GPU", "C3")
+        # slicing-by-4: 4 table lookups (4 B each) per 4 key bytes
+        lds_bytes = kb3 * 4.0
+        lds_gbs = lds_bytes / (c["kernel_ms"] * 1e-3) / 1e9
+        c["roofline_lds"] = {"bound": "lds", "achieved": round(lds_gbs, 1), "peak": LDS_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(lds_gbs / LDS_PEAK_GBS, 4), "lds_bytes_per_launch": int(lds_bytes),
+                             "note": "table reads only: 1 ds_read_b32 per key byte, near conflict-free copies"}
+        res["c3_crc32"] = c
+        m3 = leg(t, torch, "md5", keys3, off3, out3, max(5, args.steps // 2), 1, dist_on, sh3, kb3, nk3, kb3,
+                 f"C3: md5 over {n_local} x 32 B keys per GPU", "C3")
+        m3["roofline_hbm"] = m3.pop("roofline")
+        m3["roofline"] = valu_roofline(md5_ops(torch, off3), m3["kernel_ms"], ceiling)
+        res["c3_md5"] = m3
+        if sc3:
+            res["c3_scatter"] = sc3
         del keys3, off3, out3
+        torch.cuda.empty_cache()
+
+    if not args.no_extra and not args.no_c4:
+        # ---- C4 shard: 256-byte keys, one GPU's share of configs[3] (scattered from rank 0 at N > 1)
+        c4 = t.CONFIGS["C4"]["spec"]
+        n4 = args.c4_nkeys
+        keys4, off4, _, sc4 = resident(c4, n4)
+        nk4 = off4.numel() - 1
+        kb4 = int(off4[-1].item())
+        out4 = torch.empty(nk4, dtype=torch.int32, device=dev)
+        sh4 = c4.shape(kb4)
+        r4 = {"workload": f"C4 shard: {n4} x 256 B keys per GPU (BASELINE configs[3] is 2^28 keys over 8 GPUs)"}
+        for mode in ("md5", "crc32", "fnv1a_64"):
+            x = leg(t, torch, mode, keys4, off4, out4, 10, 1, dist_on, sh4, kb4, nk4, kb4, mode, "C4")
+            x.pop("workload")
+            if mode == "md5":
+                x["roofline_valu"] = valu_roofline(md5_ops(torch, off4), x["kernel_ms"], ceiling)
+            r4[mode] = x
+        if sc4:
+            r4["scatter"] = sc4
+        res["c4_shard"] = r4
+        del keys4, off4, out4
+        torch.cuda.empty_cache()
 
     # ---- redis key extraction, rank 0: 2^20 pipelined RESP GETs over
     # the first C2 keys (binary-safe), parsed on the device into the CSR above
@@ -327,6 +441,10 @@ def main():
             res["redis_key_extraction"] = redis_leg(t, torch, np, spec, dev)
         except Exception as e:  # reported beside the headline, never instead of it
             res["redis_key_extraction"] = {"error": repr(e)}
+
+    # ---- C5 pipelined GET replay through the host batch API (rank 0, N = 1)
+    if rank == 0 and world == 1 and not args.no_extra:
+        res["c5_e2e"] = c5_leg()
 
     # ---- CPU baseline (rank 0, N = 1)
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -343,11 +461,32 @@ def main():
         dist.destroy_process_group()
 
 
+def c5_leg(seconds=0.4):
+    """tools/nc_c5_replay: 64 x 128 pipelined GETs read into 16,336-byte mbufs
+    with repair, one mbuf's keys per submit_spans batch, depth 1/2/4, copy and
+    zero-copy, next to the per-key host hash of the same spans."""
+    exe = os.path.join(HERE, "tools", "nc_c5_replay")
+    if not os.path.exists(exe):
+        return {"error": "tools/nc_c5_replay not built"}
+    try:
+        p = subprocess.run([exe, str(seconds)], capture_output=True, text=True, timeout=120)
+    except Exception as e:
+        return {"error": repr(e)}
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not rows:
+        return {"error": f"rc {p.returncode}", "stderr": p.stderr[-400:]}
+    host = [r for r in rows if r["point"] == "host_per_key"]
+    gpu = [r for r in rows if r["point"] == "gpu"]
+    return {"workload": "C5: 64 connections x 128 pipelined 'get <key>\\r\\n' (Zipf 8-64 B printable keys) read "
+                        "into 16,336-byte mbufs with repair; one mbuf's keys per nc_gpuhash_submit_spans batch; "
+                        "host->device->host, fnv1a_64",
+            "host_per_key": host[0] if host else None, "gpu": gpu,
+            "mismatches": int(sum(r["mismatches"] for r in gpu))}
+
+
 def redis_leg(t, torch, np, spec, dev, nreq=1 << 20, reps=10):
     """nc_gpuhash_redis_parse_device over nreq "*2 $3 get $<len> <key>" requests
     (wall time per parse, host syncs included: the counts size the launches)."""
-    import time
-
     kh, oh = t.synth_host(spec, 0, nreq)
     kb = kh.tobytes()
     stream = b"".join(b"*2\r\n$3\r\nget\r\n$%d\r\n%s\r\n" % (int(oh[i + 1] - oh[i]), kb[int(oh[i]): int(oh[i + 1])])
