@@ -163,8 +163,11 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
                                                               uint32_t *__restrict__ out, uint64_t ntiles,
                                                               uint32_t chunk)
 {
+    /* a round consumes RB bytes of every key: one 64-byte block from
+     * registers, or (LDS) one 128-byte line from the image */
+    constexpr uint32_t RB = LDS ? 128u : 64u;
     __shared__ uint32_t tab[has_table<MODE>() ? kTabWords : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kImage : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kLineImage : 16];
     if constexpr (has_table<MODE>()) {
         for (uint32_t i = threadIdx.x; i < 4u * 256u; i += 1024u) {
             const uint32_t v = tab_entry<MODE>(i >> 8, i & 255u);
@@ -181,25 +184,25 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
     if (tile >= tlast) return;
     Walker wk;
     wk.init(keys, off, nkeys, tlast, lane);
-    uint8_t *const img = kbuf + (LDS ? wave * kImage : 0u);
+    uint8_t *const img = kbuf + (LDS ? wave * kLineImage : 0u);
 
     TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
     Offs no = wk.load_off(tile + 1u);
     u32x4 da[4], db[4];
-    if constexpr (LDS) wk.dma(cur_t, 0u, img);
+    if constexpr (LDS) wk.dma_lines(cur_t, 0u, img);
     else wk.load_regs(cur_t, 0u, da);
     uint32_t b = 0;
     uint32_t h = init_state<MODE>();
 
-    /* one round on `cur`; the next round's block goes to `nxt` (registers) or
-     * to the LDS image */
+    /* one round on `cur` (and, LDS, `nxt` as the line's second half); the
+     * next round's bytes go to `nxt` (registers) or to the LDS image */
     auto round = [&](u32x4 (&cur)[4], u32x4 (&nxt)[4]) __attribute__((always_inline)) {
-        const bool more = __ballot(cur_t.valid && cur_t.len > 64u * (b + 1u)) != 0ull;
+        const bool more = __ballot(cur_t.valid && cur_t.len > RB * (b + 1u)) != 0ull;
         const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
         if constexpr (LDS) {
-            wk.read_img(img, cur);
+            wk.read_lines(img, cur, nxt);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the image's reads are done */
-            wk.dma(more ? cur_t : nxt_t, more ? b + 1u : 0u, img);
+            wk.dma_lines(more ? cur_t : nxt_t, more ? b + 1u : 0u, img);
         } else {
             wk.load_regs(more ? cur_t : nxt_t, more ? b + 1u : 0u, nxt);
         }
@@ -207,10 +210,13 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
          * a re-read of the next tile's while this one still has blocks */
         no = wk.load_off(more ? tile + 1u : tile + 2u);
 
-        const int32_t rem = (int32_t)cur_t.len - 64 * (int32_t)b;
+        const int32_t rem = (int32_t)cur_t.len - (int32_t)RB * (int32_t)b;
         if (cur_t.valid && (rem > 0 || (b == 0u && cur_t.len == 0u))) {
             h = block_step<MODE>(h, cur, rem, tab, lane4);
-            if (rem <= 64) {
+            if constexpr (LDS) {
+                if (rem > 64) h = block_step<MODE>(h, nxt, rem - 64, tab, lane4);
+            }
+            if (rem <= (int32_t)RB) {
                 const rsrc_t rout = make_rsrc(out + tile * 64u, 256u);
                 __builtin_amdgcn_raw_buffer_store_b32(final_state<MODE>(h), rout, (int)(lane * 4u), 0, kAuxNt);
             }
@@ -225,9 +231,13 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
         }
     };
     for (;;) {
-        round(da, db);
-        if (tile >= tlast) break;
-        round(db, da);
+        if constexpr (LDS) {
+            round(da, db);
+        } else {
+            round(da, db);
+            if (tile >= tlast) break;
+            round(db, da);
+        }
         if (tile >= tlast) break;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */

@@ -33,7 +33,8 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr int kRsrcWord3 = 0x00020000; /* gfx9 raw buffer: DATA_FORMAT 32, no swizzle */
 constexpr int kAuxNt = 2;              /* slc: the streaming cache policy (nt) */
-constexpr uint32_t kImage = 64u * 64u; /* one 64-byte block of each of a tile's 64 keys */
+constexpr uint32_t kImage = 64u * 64u;      /* one 64-byte block of each of a tile's 64 keys */
+constexpr uint32_t kLineImage = 64u * 128u; /* one 128-byte line of each of a tile's 64 keys */
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void *base, uint64_t nbytes)
 {
@@ -123,6 +124,41 @@ struct Walker {
             if (rem > (int32_t)(16u * j))
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(img + 1024 * i),
                                                           16, vo + 64u * b + 16u * j, 0, 0, 0);
+        }
+    }
+
+    /* Long keys, whole lines: bytes [128b, 128b + 128) of the lanes' keys
+     * into an 8 KiB image (key k's 128 bytes at k * 128) — full 128-byte
+     * lines, so a line's two 64-byte halves are not fetched a round apart
+     * (the second fetch missed L2 three times in four: 1.74x the HBM bytes on
+     * 256-byte keys). Instruction i moves keys 8i .. 8i+7, eight lanes per
+     * key. Chunk j of key k lands in slot j ^ (k & 7) of its row, so the
+     * readers' ds_read_b128 at a 128-byte lane stride hit distinct banks. */
+    __device__ __forceinline__ void dma_lines(const TileKeys &t, uint32_t b, uint8_t *img) const
+    {
+        const rsrc_t r = make_rsrc(keys + t.s0, kbytes - t.s0);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int key = 8 * i + (int)(lane >> 3);
+            const uint32_t j = (lane & 7u) ^ ((uint32_t)key & 7u); /* the global chunk for this slot */
+            const uint32_t vo = (uint32_t)__shfl((int)t.srel, key);
+            const int32_t rem = __shfl((int)t.len, key) - 128 * (int32_t)b;
+            if (rem > (int32_t)(16u * j))
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(img + 1024 * i),
+                                                          16, vo + 128u * b + 16u * j, 0, 0, 0);
+        }
+    }
+
+    /* this lane's 128 bytes from the line image (see dma_lines) */
+    __device__ __forceinline__ void read_lines(const uint8_t *img, u32x4 (&d0)[4], u32x4 (&d1)[4]) const
+    {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint8_t *row = img + lane * 128u;
+        const uint32_t sw = lane & 7u;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            d0[c] = *reinterpret_cast<const u32x4 *>(row + 16u * ((uint32_t)c ^ sw));
+            d1[c] = *reinterpret_cast<const u32x4 *>(row + 16u * ((uint32_t)(c + 4) ^ sw));
         }
     }
 

@@ -73,6 +73,37 @@ __device__ __forceinline__ uint32_t pad_word(uint32_t d, int32_t y)
     return __builtin_amdgcn_perm(d, kPadSrc, (uint32_t)sel);
 }
 
+/* The 16 message words of a block holding m (1..64) of the key's bytes, the
+ * pad byte after them and zeros (no bit length: the caller adds it). When m
+ * is the same on every active lane (fixed-length keys) the selectors are
+ * wave-uniform and computed on the scalar unit. */
+__device__ __forceinline__ void msg_words(const u32x4 (&d)[4], int32_t m, uint32_t pad_src, uint32_t (&w)[16])
+{
+    const int32_t m0 = __builtin_amdgcn_readfirstlane(m);
+    if (__ballot(m != m0) == 0ull) {
+        const uint32_t r = (uint32_t)m0 & 3u;
+        const uint32_t bnd = r == 0u ? kBoundary0 : (r == 1u ? kBoundary1 : (r == 2u ? kBoundary2 : kBoundary3));
+        const int32_t y0 = (int32_t)bnd + (m0 >> 2) * kStep;
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            /* the clamp on the scalar unit (hipcc would use v_med3) and the
+             * selector as the perm's one SGPR operand */
+            uint32_t sel;
+            asm("s_max_i32 %0, %1, 0\n\ts_min_i32 %0, %0, %2" : "=&s"(sel) : "s"(y0 - t * kStep), "s"(kKeep));
+            w[t] = __builtin_amdgcn_perm(d[t >> 2][t & 3], pad_src, sel);
+        }
+    } else {
+        const uint32_t r = (uint32_t)m & 3u;
+        /* kBoundary[r] without branches: two 64-bit selects and a shift */
+        const uint64_t pair = (r & 2u) ? ((uint64_t)kBoundary3 << 32 | kBoundary2)
+                                       : ((uint64_t)kBoundary1 << 32 | kBoundary0);
+        const uint32_t bnd = (uint32_t)(pair >> (32u * (r & 1u)));
+        const int32_t y0 = (int32_t)bnd + (m >> 2) * kStep;
+#pragma unroll
+        for (int t = 0; t < 16; t++) w[t] = pad_word(d[t >> 2][t & 3], y0 - t * kStep);
+    }
+}
+
 /* per-wave LDS queue of keys waiting for their data-free last block */
 constexpr uint32_t kQ = 128;        /* entries per wave (>= 64 + 63) */
 constexpr uint32_t kQWords = 6;     /* A, B, C, D, length, key index */
@@ -168,32 +199,7 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
         if constexpr (LDS) wk.read_img(img, d); /* this round's block, DMA'd during the previous round */
         const u32x4 (&cur)[4] = d;
         if (act) {
-            const int32_t m = rem < 64 ? rem : 64;
-            const int32_t m0 = __builtin_amdgcn_readfirstlane(m);
-            if (__ballot(m != m0) == 0ull) {
-                /* every active lane ends at the same byte (fixed-length keys):
-                 * the selectors are wave-uniform, computed on the scalar unit */
-                const uint32_t r = (uint32_t)m0 & 3u;
-                const uint32_t bnd = r == 0u ? kBoundary0 : (r == 1u ? kBoundary1 : (r == 2u ? kBoundary2 : kBoundary3));
-                const int32_t y0 = (int32_t)bnd + (m0 >> 2) * kStep;
-#pragma unroll
-                for (int t = 0; t < 16; t++) {
-                    /* the clamp on the scalar unit (hipcc would use v_med3) and
-                     * the selector as the perm's one SGPR operand */
-                    uint32_t sel;
-                    asm("s_max_i32 %0, %1, 0\n\ts_min_i32 %0, %0, %2" : "=&s"(sel) : "s"(y0 - t * kStep), "s"(kKeep));
-                    w[t] = __builtin_amdgcn_perm(cur[t >> 2][t & 3], pad_src, sel);
-                }
-            } else {
-                const uint32_t r = (uint32_t)m & 3u;
-                /* kBoundary[r] without branches: two 64-bit selects and a shift */
-                const uint64_t pair = (r & 2u) ? ((uint64_t)kBoundary3 << 32 | kBoundary2)
-                                               : ((uint64_t)kBoundary1 << 32 | kBoundary0);
-                const uint32_t bnd = (uint32_t)(pair >> (32u * (r & 1u)));
-                const int32_t y0 = (int32_t)bnd + (m >> 2) * kStep;
-#pragma unroll
-                for (int t = 0; t < 16; t++) w[t] = pad_word(cur[t >> 2][t & 3], y0 - t * kStep);
-            }
+            msg_words(cur, rem < 64 ? rem : 64, pad_src, w);
             const bool fin = rem <= 55; /* the bit length fits behind the pad */
             if (fin) {
                 w[14] = len << 3;
@@ -260,6 +266,97 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
     while (q.count != 0u) run_tail(q, lane, out);
 }
 
+/*
+ * Long keys: the same rounds, fed from an 8 KiB LDS line image per wave
+ * (nc_direct.h dma_lines: 128 bytes of every key per round, whole lines, so a
+ * line is fetched once). A round hashes up to two blocks of each key; keys
+ * whose padding needs one more, data-free block get it in the same round
+ * (with long keys every lane of a tile usually needs it at once, so there is
+ * no queue).
+ */
+__global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__restrict__ keys,
+                                                           const uint64_t *__restrict__ off, uint64_t nkeys,
+                                                           uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t kbuf[kWaves * kLineImage];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t tile = ((uint64_t)blockIdx.x * kWaves + wave) * chunk;
+    const uint64_t tlast = ntiles < tile + chunk ? ntiles : tile + chunk;
+    if (tile >= tlast) return;
+    Walker wk;
+    wk.init(keys, off, nkeys, tlast, lane);
+    uint8_t *const img = kbuf + wave * kLineImage;
+    TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
+    Offs no = wk.load_off(tile + 1u);
+    wk.dma_lines(cur_t, 0u, img);
+    uint32_t b = 0;
+    uint32_t st[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
+    uint32_t pad_src;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(pad_src) : "i"(kPadSrc));
+
+    /* one 64-byte block holding rem (> 0) of the key's remaining bytes */
+    auto block = [&](const u32x4 (&d)[4], int32_t rem) __attribute__((always_inline)) {
+        uint32_t w[16];
+        msg_words(d, rem < 64 ? rem : 64, pad_src, w);
+        const bool fin = rem <= 55;
+        if (fin) {
+            w[14] = cur_t.len << 3;
+            w[15] = cur_t.len >> 29;
+        }
+        uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+        md5_steps(v, w, std::make_integer_sequence<int, 61>{});
+        if (fin) {
+            const rsrc_t rout = make_rsrc(out + tile * 64u, 256u);
+            __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
+        } else {
+            md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
+            st[0] += v[0];
+            st[1] += v[1];
+            st[2] += v[2];
+            st[3] += v[3];
+        }
+    };
+    for (;;) {
+        const bool more = __ballot(cur_t.valid && cur_t.len > 128u * (b + 1u)) != 0ull;
+        const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
+        u32x4 d0[4], d1[4];
+        wk.read_lines(img, d0, d1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the image's reads are done */
+        wk.dma_lines(more ? cur_t : nxt_t, more ? b + 1u : 0u, img);
+        no = wk.load_off(more ? tile + 1u : tile + 2u);
+
+        const int32_t rem = (int32_t)cur_t.len - 128 * (int32_t)b; /* key bytes from this line's start */
+        if (cur_t.valid && rem > 0) block(d0, rem);
+        if (__ballot(cur_t.valid && rem > 64) != 0ull && cur_t.valid && rem > 64) block(d1, rem - 64);
+        /* the data-free last block: length % 64 in 56..63 or 0 (or an empty
+         * key), ending in this line */
+        const int32_t last = rem > 64 ? rem - 64 : rem; /* bytes in the line's last block with data */
+        const bool tail = cur_t.valid && ((rem > 0 && rem <= 128 && last >= 56) || (b == 0u && cur_t.len == 0u));
+        if (__ballot(tail) != 0ull && tail) {
+            uint32_t w[16] = {};
+            w[0] = (cur_t.len & 63u) == 0u ? 0x80u : 0u;
+            w[14] = cur_t.len << 3;
+            w[15] = cur_t.len >> 29;
+            const rsrc_t rout = make_rsrc(out + tile * 64u, 256u);
+            __builtin_amdgcn_raw_buffer_store_b32(md5_block_final_a(st, w), rout, (int)(lane * 4u), 0, kAuxNt);
+        }
+        if (more) {
+            b++;
+        } else {
+            tile++;
+            b = 0;
+            cur_t = nxt_t;
+            st[0] = NC_MD5_A0;
+            st[1] = NC_MD5_B0;
+            st[2] = NC_MD5_C0;
+            st[3] = NC_MD5_D0;
+        }
+        if (tile >= tlast) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
+}
+
 namespace nc_md5 {
 
 /* var: bits 0-1 tiles per wave (0: 16, 1: 8, 2: 32, 3: 64); bit 2: the LDS-DMA
@@ -274,8 +371,8 @@ hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, 
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     (void)hipGetLastError();
     if (var & 4)
-        hipLaunchKernelGGL(nc_md5_direct_kernel<true>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off, nkeys,
-                           d_out, ntiles, chunk);
+        hipLaunchKernelGGL(nc_md5_lines_kernel, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off, nkeys, d_out,
+                           ntiles, chunk);
     else
         hipLaunchKernelGGL(nc_md5_direct_kernel<false>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off,
                            nkeys, d_out, ntiles, chunk);
