@@ -21,6 +21,11 @@
 #define OP_MULLO(x, y) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x) : "v"(y))
 #define OP_BFE(x, y) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(x) : "v"(y))
 #define OP_XAD(x, y) asm volatile("v_xad_u32 %0, %0, %1, %1" : "+v"(x) : "v"(y))
+#define OP_XORSDWA(x, y) asm volatile("v_xor_b32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "+v"(x) : "v"(y))
+#define OP_FNV(x, y) asm volatile("v_xor_b32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n\tv_mul_lo_u32 %0, %0, %1" : "+v"(x) : "v"(y))
+#define OP_FNVSA(x, y) asm volatile("v_xor_b32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n\tv_lshl_add_u32 v40, %0, 1, %0\n\tv_lshl_add_u32 v41, v40, 3, v40\n\tv_lshl_add_u32 %0, v41, 4, v40" : "+v"(x) : "v"(y) : "v40", "v41")
+#define OP_MULU24(x, y) asm volatile("v_mul_u32_u24_e32 %0, %1, %0" : "+v"(x) : "v"(y))
+#define OP_CNDMASK(x, y) asm volatile("v_cmp_lt_u32_e32 vcc, %0, %1\n\tv_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(y) : "vcc")
 #define OP_ADD_SGPR(x, y) asm volatile("s_mov_b32 s40, 0x12345\n\tv_add3_u32 %0, %0, %1, s40" : "+v"(x) : "v"(y) : "s40")
 
 #define KERNEL(NAME, OP)                                                                   \
@@ -50,6 +55,11 @@ KERNEL(mullo, OP_MULLO)
 KERNEL(bfe, OP_BFE)
 KERNEL(xad, OP_XAD)
 KERNEL(add3s, OP_ADD_SGPR)
+KERNEL(xorsdwa, OP_XORSDWA)
+KERNEL(fnv, OP_FNV)
+KERNEL(fnvsa, OP_FNVSA)
+KERNEL(mulu24, OP_MULU24)
+KERNEL(cndmask, OP_CNDMASK)
 
 static int g_cus;
 static unsigned *g_out;
@@ -92,5 +102,6 @@ int main()
     printf("# %s CUs %d clock %d kHz\n", p.gcnArchName, g_cus, clk);
     RUN(add) RUN(add3) RUN(alignbit) RUN(bitop3) RUN(perm) RUN(med3) RUN(xor) RUN(lshladd) RUN(mullo) RUN(bfe) RUN(xad)
     RUN(add3s)
+    RUN(xorsdwa) RUN(fnv) RUN(fnvsa) RUN(mulu24) RUN(cndmask)
     return 0;
 }
