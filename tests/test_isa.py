@@ -1,5 +1,11 @@
 """Static ISA checks of the gfx950 code object (CPU only; compiles to .s).
 
+The wave ring (nc_hash_kernel_wr) waits for its LDS-DMAs with constant
+vmcnt counts that hold only if every iteration issues the same ring
+operations in the same order: tools/check_ring.py walks every path of every
+ring instantiation and checks the counts between its waits (and a mutated
+kernel with one store removed must fail it).
+
 The register-staged kernel issues its loads in inline asm and waits with
 hand-counted vmcnt(N). tools/check_vmcnt.py walks every feasible path of the
 kernel's basic-block graph, models the in-order counter, and fails if any
@@ -95,3 +101,42 @@ def test_ring_bounds_are_not_sign_extended(asm_file):
         elif cur and "nc_hash_kernel_wr" in cur and line.strip().startswith("s_ashr_i32"):
             bad.append(cur)
     assert not bad, sorted(set(bad))[:3]
+
+
+def test_ring_vmem_counts_are_balanced(asm_file):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_ring.py"), asm_file],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-4000:]
+    n = int(r.stdout.split(" ring kernel(s)")[0].split()[-1])
+    assert n >= 100, r.stdout[-500:]  # every shape, mode and server_idx instantiation
+    assert "exploration bound" not in r.stdout
+
+
+def _one_ring_kernel(asm_file, sub="nc_hash_kernel_wrILi6ELi0ELi4ELi2ELi3ELin1ELi1ELi128"):
+    lines = open(asm_file).read().splitlines()
+    start = next(i for i, l in enumerate(lines) if l.startswith("_Z") and sub in l.split(":")[0])
+    end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
+    return lines[start:end + 1]
+
+
+@pytest.mark.parametrize("victim", ["global_store_dword", "global_load_lds_dwordx4"])
+def test_ring_checker_flags_an_unbalanced_iteration(asm_file, tmp_path, victim):
+    """drop the LAST inline-asm instance of one ring operation (a store of the
+    loop's store phase / a slab DMA of the loop's issue_slab): the iteration
+    then issues kIter - 1 ring operations and the checker must say so"""
+    body = _one_ring_kernel(asm_file)
+    asm, idx = False, []
+    for i, l in enumerate(body):
+        if ";;#ASMSTART" in l:
+            asm = True
+        elif ";;#ASMEND" in l:
+            asm = False
+        elif asm and l.strip().startswith(victim):
+            idx.append(i)
+    assert idx
+    del body[idx[-1]]
+    f = tmp_path / "mut.s"
+    f.write_text("\n".join(body) + "\n")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_ring.py"), str(f)],
+                       capture_output=True, text=True)
+    assert r.returncode == 1 and "1 ring kernel(s)" in r.stdout and "0 report(s)" not in r.stdout, r.stdout
