@@ -131,39 +131,43 @@ def test_batched_path_fails_loudly_without_gpu():
 
 
 def test_auto_policy_choices():
-    """Shape-driven pipeline choice (host logic): the register-
-    staged workgroup pipeline when the shape is unknown, oversubscribed
-    workgroup grids (and length grouping) for varying lengths, the wave ring
-    for fixed 20-40 B fnv-like keys and for long keys."""
+    """Shape-driven pipeline choice (host logic): md5 always on
+    the direct per-lane block pipeline (its LDS-DMA line image from 64-byte
+    keys); the byte-serial modes on the direct pipeline for long keys and the
+    crcs for fixed short keys; the register-staged workgroup pipeline when the
+    shape is unknown; oversubscribed workgroup grids (and length grouping) for
+    varying lengths; the wave ring for fixed 20-40 B fnv-like keys."""
     WG, RS, RING5, RING4 = 1 << 16, 32, 128 | (3 << 8), 128
-    SORTED, OVER, RING_SORTED = 1 << 17, 1 << 18, 128 | 16384
+    SORTED, OVER = 1 << 17, 1 << 18
+    DIRECT, DIRECT_LDS = 1 << 19, 4 << 20
     n = 1 << 26
     assert t.pick_variant("fnv1a_64", n) == RS
-    assert t.pick_variant("md5", n) == RS  # unknown shape
+    assert t.pick_variant("md5", n) == DIRECT  # unknown shape
     # C2 (Zipf 8-64 B, mean 19.3)
     assert t.pick_variant("fnv1a_64", n, (19 * n, 8, 64)) == WG | OVER
     assert t.pick_variant("crc32", n, (19 * n, 8, 64)) == WG | OVER
     assert t.pick_variant("one_at_a_time", n, (19 * n, 8, 64)) == WG | SORTED | OVER
-    assert t.pick_variant("md5", n, (19 * n, 8, 64)) == RING_SORTED
+    assert t.pick_variant("md5", n, (19 * n, 8, 64)) == DIRECT
     # uniform 8-64 B (mean 36)
     assert t.pick_variant("fnv1a_64", n, (36 * n, 8, 64)) == RS
-    assert t.pick_variant("md5", n, (36 * n, 8, 64)) == RS | SORTED
+    assert t.pick_variant("md5", n, (36 * n, 8, 64)) == DIRECT
     assert t.pick_variant("crc32a", n, (36 * n, 8, 64)) == RS | OVER
-    assert t.pick_variant("md5", n, (24 * n, 8, 64)) == WG | SORTED | OVER
     # C3 (fixed 32 B)
     for name in ("fnv1_64", "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == RING5, name
     for name in ("crc16", "crc32", "crc32a"):
-        assert t.pick_variant(name, n, (32 * n, 32, 32)) == WG | OVER, name
+        assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT, name
     for name in ("one_at_a_time", "jenkins"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == RS, name
-    assert t.pick_variant("md5", n, (32 * n, 32, 32)) == RS | OVER
+    assert t.pick_variant("md5", n, (32 * n, 32, 32)) == DIRECT
     # short fixed, long keys (C4)
     assert t.pick_variant("fnv1a_64", n, (8 * n, 8, 8)) == WG
-    assert t.pick_variant("md5", n, (16 * n, 16, 16)) == WG | OVER
-    assert t.pick_variant("crc32", n >> 3, (256 * (n >> 3), 256, 256)) == RING4
-    assert t.pick_variant("md5", n >> 3, (256 * (n >> 3), 256, 256)) == RING5
-    assert t.pick_variant("md5", n >> 3, (128 * (n >> 3), 128, 128)) == WG | OVER
+    assert t.pick_variant("md5", n, (16 * n, 16, 16)) == DIRECT
+    for name in ("crc32", "fnv1a_64", "one_at_a_time", "crc16", "fnv1_32"):
+        assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS, name
+    assert t.pick_variant("md5", n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS
+    assert t.pick_variant("md5", n >> 3, (128 * (n >> 3), 128, 128)) == DIRECT | DIRECT_LDS
+    assert t.pick_variant("murmur", n >> 3, (256 * (n >> 3), 256, 256)) == RING4
     assert t.pick_variant("hsieh", 1000, (100000, 100, 100)) == RING5
     assert t.pick_variant("fnv1a_64", 0, (0, 0, 0)) == RS
     assert L.lib().nc_gpuhash_pick_variant(12, n, None) == -1
