@@ -260,7 +260,7 @@ def test_key_buffers_beyond_4gib(gpu):
     host = {i: t.synth_host(spec, i, 1)[0][:256].tobytes() for i in sample}
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     try:
-        for var in (0, 65536, 32, 128, 896, 2176):
+        for var in (0, 65536, 32, 128, 896, 2176, 1 << 19, (1 << 19) | (4 << 20)):
             L.lib().nc_gpuhash_set_tuning(0, 0, var)
             for name in ("md5", "crc32", "fnv1a_64"):
                 t.hash_batch_device(name, kd, od, out, shape=spec.shape(256 * n))
@@ -280,6 +280,45 @@ def test_key_buffers_beyond_4gib(gpu):
             hv = t.hash_key("fnv1a_64", host[i])
             p = int(np.searchsorted(vals, hv, side="left")) % 8
             assert int(g[i]) == p % 4, (shape, i)
+    del kd, od, out
+    torch.cuda.empty_cache()
+
+
+def test_c4_full_shard(gpu, digests):
+    """One GPU's whole C4 shard (BASELINE configs[3]: keys [0, 2^25) of the
+    2^28 x 256 B set, 8 GiB, offsets past 2^31, 2^32 and 2^33): md5 and crc32
+    (the C4 modes) and fnv1a_64 through the auto policy (the direct line-image
+    pipelines) and the direct register path; the first 2^20 hashes against
+    the reference's digest of the C4 prefix, sampled keys around every 2 GiB
+    mark and at random against the per-key host symbols."""
+    import torch
+
+    d = digests["C4_prefix_2^20"]
+    spec = t.SynthSpec(**d["spec"])
+    n = 1 << 25
+    kd, od = t.synth_device(spec, 0, n)
+    assert int(od[-1].item()) == 256 * n
+    rng = np.random.default_rng(25)
+    marks = [(1 << 23) * j for j in range(1, 5)]  # 2, 4, 6, 8 GiB
+    sample = sorted({0, n - 1} | {m + e for m in marks for e in (-1, 0, 1) if 0 <= m + e < n} |
+                    {int(x) for x in rng.integers(0, n, size=64)})
+    host = {i: t.synth_host(spec, i, 1)[0][:256].tobytes() for i in sample}
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    try:
+        for var in (0, 1 << 19):
+            L.lib().nc_gpuhash_set_tuning(0, 0, var)
+            for name in ("md5", "crc32", "fnv1a_64"):
+                out.fill_(0)
+                t.hash_batch_device(name, kd, od, out, shape=spec.shape(256 * n))
+                torch.cuda.synchronize()
+                h = out.cpu().numpy().view(np.uint32)
+                if name in d["modes"]:
+                    assert h[:8].tolist() == d["modes"][name]["head"], (var, name)
+                    assert sha(h[: d["nkeys"]]) == d["modes"][name]["sha256"], (var, name)
+                for i in sample:
+                    assert int(h[i]) == t.hash_key(name, host[i]), (var, name, i)
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
     del kd, od, out
     torch.cuda.empty_cache()
 
