@@ -1,9 +1,11 @@
 #!/bin/bash
 # Round profile: bench line, rocprofv3 kernel-trace stats of the SAME bench
 # command, FETCH_SIZE / WRITE_SIZE passes (one counter per rocprofv3 run,
-# nothing else traced) for C2/C3 x fnv1a_64/md5, and the end-to-end host
-# batch benchmark. Every GPU step has its own limit; the first failure ends
-# the script.     usage: tools/gpu_profile_round.sh <tag>
+# nothing else traced) for every bench leg's hash kernel (C2 fnv1a_64 / md5 /
+# server_idx, C3 fnv1a_64 / crc32 / md5, C4 shard md5 / crc32 / fnv1a_64), the
+# end-to-end host batch benchmark and the C5 replay. Every GPU step has its own limit; the first failure ends
+# the script.     usage: tools/gpu_profile_round.sh <tag> [bench|pmc]   (default: both;
+# the parts fit one gpurun call each)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -20,15 +22,25 @@ step() {  # name limit cmd...
     return $rc
 }
 
+PART=${2:-all}
+if [ "$PART" != pmc ]; then
 step bench 600 python3 bench.py || exit $?
 grep '^{' "$OUT/bench.log" > "$OUT/bench.json"
 step rocprof_bench 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
     python3 bench.py || exit $?
 grep '^{' "$OUT/rocprof_bench.log" > "$OUT/bench_under_rocprof.json"
-for cfg in C2 C3; do for mode in fnv1a_64 md5; do for ctr in FETCH_SIZE WRITE_SIZE; do
-    step "pmc_${cfg}_${mode}_${ctr}" 300 rocprofv3 --pmc $ctr -d "$OUT/pmc_${cfg}_${mode}_${ctr}" -o pmc \
-        --output-format csv -- python3 tools/pmc_run.py --config $cfg --mode $mode --variant 0:0:0 --iters 5 || exit $?
-done; done; done
+fi
+[ "$PART" = bench ] && { echo done; exit 0; }
+for cm in C2:fnv1a_64 C2:md5 C2:server_idx C3:fnv1a_64 C3:crc32 C3:md5 C4S:md5 C4S:crc32 C4S:fnv1a_64; do
+    cfg=${cm%%:*}; mode=${cm#*:}
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+        step "pmc_${cfg}_${mode}_${ctr}" 300 rocprofv3 --pmc $ctr -d "$OUT/pmc_${cfg}_${mode}_${ctr}" -o pmc \
+            --output-format csv -- python3 tools/pmc_run.py --config $cfg --mode $mode --variant 0:0:0 --iters 5 \
+            || exit $?
+    done
+done
 step e2e 400 tools/nc_e2e_bench 1.5 || exit $?
 grep '^{' "$OUT/e2e.log" > "$OUT/e2e.jsonl"
+step c5 300 tools/nc_c5_replay 1.0 || exit $?
+grep '^{' "$OUT/c5.log" > "$OUT/c5.jsonl"
 echo done

@@ -26,7 +26,17 @@ from pmc_summary import counters  # noqa: E402
 
 # bench.py's launch order on one GPU: (label, timed launches) -- see bench.py main(). Each phase
 # starts with a time-bounded untimed spin-up and W warm-ups, so only its last `timed` dispatches count.
-BENCH_PHASES = [("C2 fnv1a_64", 20), ("C2 md5", 5), ("C2 server_idx ketama", 5), ("C3 fnv1a_64", 20)]
+BENCH_PHASES = [("C2 fnv1a_64", 20), ("C2 md5", 10), ("C2 server_idx ketama", 10), ("C3 fnv1a_64", 20),
+                ("C3 crc32", 20), ("C3 md5", 10), ("C4 md5", 10), ("C4 crc32", 10), ("C4 fnv1a_64", 10)]
+# the PMC passes of tools/gpu_profile_round.sh: (config dir name, bench workload key, mode)
+PMC_LEGS = [("C2", "C2", "fnv1a_64"), ("C2", "C2", "md5"), ("C2", "C2", "server_idx"), ("C3", "C3", "fnv1a_64"),
+            ("C3", "C3", "crc32"), ("C3", "C3", "md5"), ("C4S", "C4", "md5"), ("C4S", "C4", "crc32"),
+            ("C4S", "C4", "fnv1a_64")]
+HASH_KERNELS = ("nc_hash_kernel", "nc_md5_", "nc_bytes_direct")
+
+
+def is_hash_kernel(name):
+    return any(k in name for k in HASH_KERNELS)
 
 
 def hash_phases(trace_csv):
@@ -36,7 +46,7 @@ def hash_phases(trace_csv):
     runs, cur = [], None
     for r in rows:
         name = r["Kernel_Name"]
-        if "nc_hash_kernel" in name:
+        if is_hash_kernel(name):
             short = name.replace("void (anonymous namespace)::", "").split("(")[0]
             if cur is None or cur["kernel"] != short:
                 cur = {"kernel": short, "ns": []}
@@ -107,8 +117,13 @@ def main():
     runs = hash_phases(os.path.join(prof, "bench_kernel_trace.csv"))
     if len(runs) != len(BENCH_PHASES):
         raise SystemExit(f"expected {len(BENCH_PHASES)} hash-kernel phases, found {len(runs)}")
-    event_ms = {"C2 fnv1a_64": under["kernel_ms_rank0"], "C3 fnv1a_64": under["c3_fnv1a_64"]["kernel_ms"],
-                "C2 server_idx ketama": under["server_idx_ketama"]["kernel_ms"]}
+    event_ms = {"C2 fnv1a_64": under["kernel_ms_rank0"], "C2 md5": under["md5"]["kernel_ms"],
+                "C2 server_idx ketama": under["server_idx_ketama"]["kernel_ms"],
+                "C3 fnv1a_64": under["c3_fnv1a_64"]["kernel_ms"], "C3 crc32": under["c3_crc32"]["kernel_ms"],
+                "C3 md5": under["c3_md5"]["kernel_ms"]}
+    for m in ("md5", "crc32", "fnv1a_64"):
+        if "c4_shard" in under:
+            event_ms[f"C4 {m}"] = under["c4_shard"][m]["kernel_ms"]
     phases = []
     for (label, timed), run in zip(BENCH_PHASES, runs):
         ns = run["ns"]
@@ -130,27 +145,29 @@ def main():
                    "of a 16-B/lane stream, MI355X_MICROARCH.md HBM section), hbm_write = WRITE_SIZE x 1024; "
                    "one counter per rocprofv3 pass; inputs as bench.py (tools/pmc_run.py, variant 0:0:0)",
            "workloads": {}}
-    for cfg in ("C2", "C3"):
-        for mode in ("fnv1a_64", "md5"):
-            rec = {}
-            for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-                d = os.path.join(src, f"pmc_{cfg}_{mode}_{ctr}", "pmc_counter_collection.csv")
-                if not os.path.exists(d):
-                    continue
-                for k, v in counters(d).items():
-                    if k.startswith("nc_hash_kernel"):
-                        rec["kernel"] = k
-                        rec[ctr + "_KB"] = v[ctr]
-                        rec["dispatches"] = v["_dispatches"]
-            if "FETCH_SIZE_KB" in rec and "WRITE_SIZE_KB" in rec:
-                rd = 2.0 * rec["FETCH_SIZE_KB"] * 1024.0
-                wr = rec["WRITE_SIZE_KB"] * 1024.0
-                rec.update(hbm_read_bytes=round(rd), hbm_write_bytes=round(wr), hbm_bytes_per_launch=round(rd + wr))
-                pmc["workloads"].setdefault(cfg, {})[mode] = rec
+    for cdir, cfg, mode in PMC_LEGS:
+        rec = {}
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(src, f"pmc_{cdir}_{mode}_{ctr}", "pmc_counter_collection.csv")
+            if not os.path.exists(d):
+                continue
+            hk = {k: v for k, v in counters(d).items() if is_hash_kernel(k)}
+            if not hk:
+                continue
+            k, v = max(hk.items(), key=lambda kv: kv[1]["_dispatches"])  # the leg's kernel (5 launches)
+            rec["kernel"] = k
+            rec[ctr + "_KB"] = v[ctr]
+            rec["dispatches"] = v["_dispatches"]
+        if "FETCH_SIZE_KB" in rec and "WRITE_SIZE_KB" in rec:
+            rd = 2.0 * rec["FETCH_SIZE_KB"] * 1024.0
+            wr = rec["WRITE_SIZE_KB"] * 1024.0
+            rec.update(hbm_read_bytes=round(rd), hbm_write_bytes=round(wr), hbm_bytes_per_launch=round(rd + wr))
+            pmc["workloads"].setdefault(cfg, {})[mode] = rec
     json.dump(pmc, open(os.path.join(dst, f"pmc_{rnd}.json"), "w"), indent=1)
-    e2e = os.path.join(src, "e2e.jsonl")
-    if os.path.exists(e2e):
-        shutil.copy(e2e, os.path.join(dst, f"{rnd}_e2e.jsonl"))
+    for name in ("e2e", "c5"):
+        f = os.path.join(src, f"{name}.jsonl")
+        if os.path.exists(f):
+            shutil.copy(f, os.path.join(dst, f"{rnd}_{name}.jsonl"))
     print(json.dumps(phases, indent=1))
     print(json.dumps(pmc["workloads"], indent=1))
 

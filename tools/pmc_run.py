@@ -26,16 +26,29 @@ def main():
     import twemproxy_amd as t
     from twemproxy_amd import _lib as L
 
-    cfg = t.CONFIGS[args.config]
+    if args.config == "C4S":  # one GPU's C4 shard, as bench.py's c4_shard leg
+        cfg = {"spec": t.CONFIGS["C4"]["spec"], "nkeys": 1 << 25}
+    else:
+        cfg = t.CONFIGS[args.config]
     n = args.nkeys or cfg["nkeys"]
     keys, off = t.synth_device(cfg["spec"], 0, n)
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     g, s, v = (int(x) for x in args.variant.split(":"))
     L.lib().nc_gpuhash_set_tuning(g, s, v)
-    shape = cfg["spec"].shape(int(off[-1].item()))  # as bench.py: the auto policy's pipeline
+    kb = int(off[-1].item())
+    shape = cfg["spec"].shape(kb)  # as bench.py: the auto policy's pipeline
     for mode in args.mode.split(","):
         for _ in range(args.iters):
-            t.hash_batch_device(mode, keys, off, out, shape=shape)
+            if mode == "server_idx":  # bench.py's fused leg: fnv1a_64 + ketama over 8 x 160 points
+                import numpy as np
+
+                rng = np.random.default_rng(9)
+                cvals = np.sort(rng.integers(0, 1 << 32, size=8 * 160, dtype=np.uint64)).astype(np.uint32)
+                cidx = rng.integers(0, 8, size=cvals.size).astype(np.uint32)
+                cont = t.continuum_device(cidx, cvals)
+                t.server_idx_device("fnv1a_64", "ketama", keys, off, cont, 8, out=out, shape=shape, key_end=kb)
+            else:
+                t.hash_batch_device(mode, keys, off, out, shape=shape, key_end=kb)
     torch.cuda.synchronize()
     print(f"{args.config} {args.mode} {args.variant} n={n} key_bytes={int(off[-1].item())}")
 
