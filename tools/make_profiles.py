@@ -78,19 +78,26 @@ def modes(src, rnd):
         key = f"grid{r['grid_cap']}_sort{r['sort']}_var{r['var']}"
         m = res["modes"].setdefault(r["mode"], {"sweep_ms_median": {}})
         m["sweep_ms_median"][key] = r["ms_median"]
+    def mode_of_kernel(name):
+        """hash mode of a kernel name: the first template argument, or md5 for its own kernels"""
+        if "nc_md5_" in name:
+            return "md5"
+        mm = re.search(r"(?:nc_hash_kernel(?:_rs|_wr)?|nc_bytes_direct_kernel)<(?:mode=)?(\d+)", name)
+        return MODE_NAMES[int(mm.group(1))] if mm else None
+
     stats = os.path.join(src, "trace", "modes_kernel_stats.csv")
     for r in csv.DictReader(open(stats)):
-        mm = re.search(r"(nc_hash_kernel(?:_rs|_wr)?)<(\d+), ([^>]*)>", r["Name"])
-        if mm:
-            name = MODE_NAMES[int(mm.group(2))]
-            res["modes"][name]["trace_kernel"] = f"{mm.group(1)}<{mm.group(2)}, {mm.group(3)}>"
+        name = mode_of_kernel(r["Name"])
+        if name:
+            res["modes"][name]["trace_kernel"] = r["Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+            res["modes"][name]["trace_kernel"] = res["modes"][name]["trace_kernel"].split("(")[0]
             res["modes"][name]["trace_avg_ms_auto"] = round(float(r["AverageNs"]) / 1e6, 4)
             res["modes"][name]["trace_calls"] = int(r["Calls"])
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         for k, v in counters(os.path.join(src, f"pmc_{ctr}", "pmc_counter_collection.csv")).items():
-            mm = re.search(r"mode=(\d+)", k)
-            if mm:
-                res["modes"][MODE_NAMES[int(mm.group(1))]][ctr + "_KB"] = v[ctr]
+            name = mode_of_kernel(k)
+            if name:
+                res["modes"][name][ctr + "_KB"] = v[ctr]
     for name, m in res["modes"].items():
         v0 = m["sweep_ms_median"].get("grid0_sort0_var0")  # var 0 = the shape policy's choice
         if v0:
