@@ -42,11 +42,22 @@ def pools(dist_fixture):
         yield p, len(p["names"])
 
 
+@pytest.mark.parametrize("pipe", [0, 1 << 28, 1 << 29], ids=["policy", "ring", "workgroup"])
 @pytest.mark.parametrize("wide", [False, True], ids=["narrow", "wide"])
 @pytest.mark.parametrize("tag", [None, b"{}", b"::"], ids=["notag", "braces", "colons"])
-def test_server_idx_matches_oracle(gpu, oracle, dist_fixture, tag, wide):
+def test_server_idx_matches_oracle(gpu, oracle, dist_fixture, tag, wide, pipe):
     import torch
 
+    from twemproxy_amd import _lib as L
+
+    L.lib().nc_gpuhash_set_tuning(0, 0, pipe)  # bit 28: wave ring, bit 29: workgroup pipeline
+    try:
+        _server_idx_vs_oracle(torch, oracle, dist_fixture, tag, wide)
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
+def _server_idx_vs_oracle(torch, oracle, dist_fixture, tag, wide):
     rng = np.random.default_rng(17)
     keyset = tagged_keyset(rng, 5000)
     keys, off = t.pack_keys(keyset)

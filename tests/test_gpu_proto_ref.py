@@ -49,20 +49,27 @@ def test_mc_parser_matches_reference(gpu):
     assert nk > 1000
 
 
+@pytest.mark.parametrize("pipe", [0, 1 << 28, 1 << 29], ids=["policy", "ring", "workgroup"])
 @pytest.mark.parametrize("wide", [False, True], ids=["narrow", "wide"])
-def test_server_idx_matches_reference(gpu, dist_fixture, wide):
+def test_server_idx_matches_reference(gpu, dist_fixture, wide, pipe):
     import torch
+
+    from twemproxy_amd import _lib as L
 
     keys, off = t.pack_keys(P.keys_of(DOC))
     buf = torch.zeros(keys.size + 64, dtype=torch.uint8, device="cuda")
     buf[: keys.size] = torch.from_numpy(keys).cuda()
     od = torch.from_numpy(off.astype(np.int64)).cuda()
     shape = (21 * (off.size - 1), 0, 64) if wide else None
-    for c, p, vals, idx in P.server_idx_cases(DOC, dist_fixture):
-        cd = t.continuum_device(idx, vals) if vals is not None else t.continuum_device(idx)
-        dist = t.DIST_NAMES[c["dist"]]
-        got = t.server_idx_device(c["mode"], dist, buf, od, cd, len(p["names"]), hash_tag=c["tag"].encode() or None,
-                                  shape=shape)
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), np.array(c["idx"], np.uint32),
-                                      err_msg=f"mode {c['mode']} {dist} tag {c['tag']!r}")
+    L.lib().nc_gpuhash_set_tuning(0, 0, pipe)  # bit 28: wave ring, bit 29: workgroup pipeline
+    try:
+        for c, p, vals, idx in P.server_idx_cases(DOC, dist_fixture):
+            cd = t.continuum_device(idx, vals) if vals is not None else t.continuum_device(idx)
+            dist = t.DIST_NAMES[c["dist"]]
+            got = t.server_idx_device(c["mode"], dist, buf, od, cd, len(p["names"]),
+                                      hash_tag=c["tag"].encode() or None, shape=shape)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), np.array(c["idx"], np.uint32),
+                                          err_msg=f"mode {c['mode']} {dist} tag {c['tag']!r} pipe {pipe}")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""In-process A/B of the fused server_pool_idx pipelines (wave ring vs
+workgroup) with a key-for-key comparison between them.
+
+    python tools/ab_sidx.py --configs C2,C3 --modes fnv1a_64,md5 --tags none,{}
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+PIPES = {"policy": 0, "ring": 1 << 28, "workgroup": 1 << 29}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C2")
+    ap.add_argument("--modes", default="fnv1a_64")
+    ap.add_argument("--dists", default="ketama,modula")
+    ap.add_argument("--tags", default="none")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import twemproxy_amd as t
+    from twemproxy_amd import _lib as L
+
+    rng = np.random.default_rng(9)
+    cvals = np.sort(rng.integers(0, 1 << 32, size=8 * 160, dtype=np.uint64)).astype(np.uint32)
+    cidx = rng.integers(0, 8, size=cvals.size).astype(np.uint32)
+    conts = {"ketama": t.continuum_device(cidx, cvals), "modula": t.continuum_device(np.arange(8, dtype=np.uint32))}
+    for cfg in args.configs.split(","):
+        spec, n = t.CONFIGS[cfg]["spec"], t.CONFIGS[cfg]["nkeys"]
+        keys, off = t.synth_device(spec, 0, n)
+        kb = int(off[-1].item())
+        shape = spec.shape(kb)
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        for mode in args.modes.split(","):
+            for dist in args.dists.split(","):
+                for tag in args.tags.split(","):
+                    tg = None if tag == "none" else tag.encode()
+
+                    def launch():
+                        t.server_idx_device(mode, dist, keys, off, conts[dist], 8, hash_tag=tg, out=out,
+                                            shape=shape, key_end=kb)
+                    ref, res = None, {}
+                    for name, v in PIPES.items():
+                        L.lib().nc_gpuhash_set_tuning(0, 0, v)
+                        out.fill_(-1)
+                        launch()
+                        torch.cuda.synchronize()
+                        h = out.cpu().numpy().copy()
+                        if ref is None:
+                            ref = h
+                            chk = "ref"
+                        else:
+                            d = np.flatnonzero(h != ref)
+                            chk = "same" if d.size == 0 else f"DIFF {d.size} first {int(d[0])}"
+                        ms = []
+                        for _ in range(args.rounds):
+                            for _ in range(3):
+                                launch()
+                            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                            e0.record()
+                            for _ in range(args.iters):
+                                launch()
+                            e1.record()
+                            torch.cuda.synchronize()
+                            ms.append(e0.elapsed_time(e1) / args.iters)
+                        res[name] = (round(statistics.median(ms), 4), chk)
+                    L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+                    alg = kb + 12.0 * n
+                    print(json.dumps({"config": cfg, "mode": mode, "dist": dist, "tag": tag,
+                                      "ms": {k: v[0] for k, v in res.items()},
+                                      "frac": {k: round(alg / v[0] / 1e6 / 8000.0, 4) for k, v in res.items()},
+                                      "check": {k: v[1] for k, v in res.items()}}), flush=True)
+        del keys, off, out
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

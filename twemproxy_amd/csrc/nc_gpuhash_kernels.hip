@@ -537,6 +537,160 @@ __device__ __forceinline__ void full_barrier()
     asm volatile("" ::: "memory");
 }
 
+constexpr int kDistNone = -1, kDistKetama = 0, kDistModula = 1, kDistPre = 3;
+
+/* server_pool_idx parameters of one launch (ignored for kDistNone) */
+struct WrDist {
+    const uint32_t *cont; /* struct continuum {index, value} pairs (src/nc_server.h:64-67) */
+    uint32_t ncont;
+    uint32_t tag;         /* hash_tag c0 | c1 << 8 | 1 << 16, or 0 for none */
+};
+
+/* hash_tag trimming of server_pool_idx (src/nc_server.c:665-677): the first
+ * c0, then the first c1 after it; with at least one byte between them the
+ * key becomes the bytes in between. Four bytes at a time: a byte equal to c
+ * is a zero byte of w ^ c*0x01010101, found with the carry-free zero-byte
+ * test (x - 0x01010101) & ~x & 0x80808080, whose lowest set bit is exact
+ * (borrows only reach bytes above a true zero), then v_ffbl. */
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x)
+{
+    return (x - 0x01010101u) & ~x & 0x80808080u;
+}
+
+template <class Src>
+__device__ __forceinline__ void tag_trim(const Src &src, typename Src::pos_t &p, uint32_t &len, uint32_t c0,
+                                         uint32_t c1)
+{
+    QStream<Src> st;
+    st.init(src, p);
+    const uint32_t p0 = c0 * 0x01010101u, p1 = c1 * 0x01010101u;
+    uint32_t s = 0xffffffffu, e = 0xffffffffu;
+    for (uint32_t i = 0; i < len; i += 8u) {
+        const uint2 w2 = st.next8();
+#pragma unroll
+        for (uint32_t h = 0; h < 2u; h++) {
+            const uint32_t w = h ? w2.y : w2.x;
+            const uint32_t base = i + 4u * h;
+            const uint32_t lim = len > base ? len - base : 0u; /* key bytes in this word */
+            const uint32_t valid = lim >= 4u ? 0x80808080u : ((1u << (8u * lim)) - 1u) & 0x80808080u;
+            const uint32_t m0 = zero_bytes(w ^ p0) & valid;
+            uint32_t m1 = zero_bytes(w ^ p1) & valid;
+            if (s == 0xffffffffu) {
+                if (m0 != 0u) {
+                    const uint32_t b0 = __builtin_ctz(m0); /* bit 7 of the first c0 byte */
+                    s = base + (b0 >> 3);
+                    m1 &= ~((2u << b0) - 1u); /* c1 strictly after it */
+                } else {
+                    m1 = 0u;
+                }
+            }
+            if (e == 0xffffffffu && m1 != 0u) e = base + (__builtin_ctz(m1) >> 3);
+        }
+    }
+    if (s != 0xffffffffu && e != 0xffffffffu && e - s > 1u) {
+        p += s + 1u;
+        len = e - s - 1u;
+    }
+}
+
+/* ketama_dispatch (src/hashkit/nc_ketama.c:222-246): the first point whose
+ * value is >= hash, wrapping to the first point; c = {index, value} pairs */
+__device__ __forceinline__ uint32_t ketama_find(const uint32_t *c, uint32_t n, uint32_t h)
+{
+    uint32_t lo = 0, len = n;
+    while (len > 0u) {
+        const uint32_t half = len >> 1;
+        if (c[2u * (lo + half) + 1u] < h) {
+            lo += half + 1u;
+            len -= half + 1u;
+        } else {
+            len = half;
+        }
+    }
+    return c[2u * (lo == n ? 0u : lo)];
+}
+
+/* ketama_find narrowed by a 256-bucket index over the top hash byte:
+ * bkt[b] = first point with value >= b << 24 (bkt[256] = n), so the answer
+ * for h lies in [bkt[h >> 24], bkt[(h >> 24) + 1]] and the search takes
+ * ~log2(n / 256) + 1 steps instead of log2(n) */
+__device__ __forceinline__ uint32_t ketama_find_bkt(const uint32_t *c, const uint32_t *bkt, uint32_t n, uint32_t h)
+{
+    const uint32_t b = h >> 24;
+    uint32_t lo = bkt[b], len = bkt[b + 1u] - lo;
+    while (len > 0u) {
+        const uint32_t half = len >> 1;
+        if (c[2u * (lo + half) + 1u] < h) {
+            lo += half + 1u;
+            len -= half + 1u;
+        } else {
+            len = half;
+        }
+    }
+    return c[2u * (lo == n ? 0u : lo)];
+}
+
+/* lower bound of v over the continuum values (no wrap) */
+__device__ __forceinline__ uint32_t cont_lower_bound(const uint32_t *c, uint32_t n, uint32_t v)
+{
+    uint32_t lo = 0, len = n;
+    while (len > 0u) {
+        const uint32_t half = len >> 1;
+        if (c[2u * (lo + half) + 1u] < v) {
+            lo += half + 1u;
+            len -= half + 1u;
+        } else {
+            len = half;
+        }
+    }
+    return lo;
+}
+
+/* server_pool_idx on the workgroup pipeline (VAR bits 12-13: 1 ketama, 2
+ * modula): hash_tag trim, hash 0 for an empty key (src/nc_server.c:639-641),
+ * then the dispatch over the continuum in global memory (L2-resident: 8 B
+ * per point); ketama narrows its binary search with the 256-entry bucket
+ * index bkt (LDS): the answer for h lies in [bkt[h >> 24], bkt[(h >> 24) + 1]]
+ * (bkt[256] = n is implicit). */
+template <int VAR>
+constexpr int wg_dist()
+{
+    return ((VAR >> 12) & 3) == 1 ? kDistKetama : ((VAR >> 12) & 3) == 2 ? kDistModula : kDistNone;
+}
+
+template <int MODE, int VAR, class Src>
+__device__ __forceinline__ uint32_t wg_value(const Src &src, typename Src::pos_t p, uint32_t len,
+                                             const uint32_t *tab, const uint32_t *bkt, const WrDist &dist)
+{
+    constexpr int D = wg_dist<VAR>();
+    if constexpr (D == kDistNone) {
+        return hash_key<MODE, VAR>(src, p, len, tab);
+    } else {
+        if (dist.tag != 0u) tag_trim(src, p, len, dist.tag & 0xffu, (dist.tag >> 8) & 0xffu);
+        uint32_t h = 0u;
+        if (len != 0u) h = hash_key<MODE, VAR>(src, p, len, tab);
+        const uint32_t *c = dist.cont;
+        const uint32_t n = dist.ncont;
+        if constexpr (D == kDistModula) {
+            return c[2u * (h % n)]; /* nc_modula.c:153 */
+        } else { /* ketama_dispatch, nc_ketama.c:222-246 */
+            const uint32_t b = h >> 24;
+            uint32_t lo = bkt[b];
+            uint32_t cnt = (b == 255u ? n : bkt[b + 1u]) - lo;
+            while (cnt > 0u) {
+                const uint32_t half = cnt >> 1;
+                if (c[2u * (lo + half) + 1u] < h) {
+                    lo += half + 1u;
+                    cnt -= half + 1u;
+                } else {
+                    cnt = half;
+                }
+            }
+            return c[2u * (lo == n ? 0u : lo)];
+        }
+    }
+}
+
 /* This lane's key [s, e) of a tile, loaded one tile ahead of its use: only
  * the LOW dwords of the u64 offsets, since every use is 32-bit (the length,
  * and the start relative to a slab base < 4 GiB away). Loads are clamped so
@@ -669,7 +823,7 @@ template <int MODE, bool SORT, int VAR>
 __global__ __launch_bounds__(kBlock, kMinWaves<MODE>()) void nc_hash_kernel(const uint8_t *__restrict__ keys_base,
                                                          const uint64_t *__restrict__ off, uint64_t delta,
                                                          uint64_t nkeys, uint32_t *__restrict__ out,
-                                                         uint64_t ntiles)
+                                                         uint64_t ntiles, WrDist dist)
 {
     /* VAR bits 1-2: L2-prefetch distance code (0 off, 1..3 -> 2..4 tiles ahead) */
     constexpr uint32_t PD = ((VAR >> 1) & 3) ? (uint32_t)((VAR >> 1) & 3) + 1u : 0u;
@@ -701,7 +855,11 @@ __global__ __launch_bounds__(kBlock, kMinWaves<MODE>()) void nc_hash_kernel(cons
     };
 
     if constexpr (uses_crc_table<MODE>()) {
+        static_assert(!uses_crc_table<MODE>() || wg_dist<VAR>() == kDistNone, "crc modes dispatch on the wave ring");
         tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
+    }
+    if constexpr (wg_dist<VAR>() == kDistKetama) { /* the bucket index, in the crc table's place */
+        tab[t] = cont_lower_bound(dist.cont, dist.ncont, t << 24);
     }
     if constexpr (SORT) {
         if (t < 2u * kBuckets) hist2[t] = 0;
@@ -837,10 +995,10 @@ __global__ __launch_bounds__(kBlock, kMinWaves<MODE>()) void nc_hash_kernel(cons
                 h = pos ^ klen_my;
             } else if (in_lds) {
                 LdsSrc src{reinterpret_cast<const uint32_t *>(slab)};
-                h = hash_key<MODE, VAR>(src, pos, klen_my, tab);
+                h = wg_value<MODE, VAR>(src, pos, klen_my, tab, tab, dist);
             } else {
                 GlobalSrc src{reinterpret_cast<const uint32_t *>(keys_base)};
-                h = hash_key<MODE, VAR>(src, myS16 + pos, klen_my, tab);
+                h = wg_value<MODE, VAR>(src, myS16 + pos, klen_my, tab, tab, dist);
                 /* retire the reader's look-ahead load here, so no register
                  * write is left pending where the two paths merge (the
                  * compiler would otherwise wait vmcnt(0) after the merge,
@@ -1026,7 +1184,7 @@ template <int MODE, bool SORT, int VAR>
 __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__restrict__ keys_base,
                                                             const uint64_t *__restrict__ off, uint64_t delta,
                                                             uint64_t nkeys, uint32_t *__restrict__ out,
-                                                            uint64_t ntiles)
+                                                            uint64_t ntiles, WrDist)
 {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kRsSmem];
     uint8_t *slab = smem;
@@ -1191,15 +1349,6 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_rs(const uint8_t *__res
  * workgroup share the crc table and the continuum; each owns its ring.
  */
 constexpr int kWrTile = 128; /* keys per wave tile (64: one key per lane, the short-key shape) */
-constexpr int kDistNone = -1, kDistKetama = 0, kDistModula = 1, kDistPre = 3;
-
-/* server_pool_idx parameters of one launch (ignored for kDistNone) */
-struct WrDist {
-    const uint32_t *cont; /* struct continuum {index, value} pairs (src/nc_server.h:64-67) */
-    uint32_t ncont;
-    uint32_t tag;         /* hash_tag c0 | c1 << 8 | 1 << 16, or 0 for none */
-};
-
 /* TK = 256 (four keys per lane) sorts the tile's keys by length inside the
  * wave and hashes them in four rounds of 64 similar lengths: a round runs as
  * long as its longest key, so Zipf lengths cost ~the sum of the four quartile
@@ -1278,85 +1427,6 @@ __device__ __forceinline__ void wr_bounds(const uint32_t *ob, uint64_t delta, ui
     const uint32_t e_hi = (uint32_t)__builtin_amdgcn_readfirstlane(ob[2 * TK + 1]);
     S = (((uint64_t)s_hi << 32) | s_lo) + delta;
     E = (((uint64_t)e_hi << 32) | e_lo) + delta;
-}
-
-/* hash_tag trimming of server_pool_idx (src/nc_server.c:665-677): the first
- * c0, then the first c1 after it; with at least one byte between them the
- * key becomes the bytes in between. */
-template <class Src>
-__device__ __forceinline__ void tag_trim(const Src &src, typename Src::pos_t &p, uint32_t &len, uint32_t c0,
-                                         uint32_t c1)
-{
-    QStream<Src> st;
-    st.init(src, p);
-    uint32_t s = 0xffffffffu, e = 0xffffffffu;
-    for (uint32_t i = 0; i < len; i += 8u) {
-        const uint2 w = st.next8();
-#pragma unroll
-        for (uint32_t b = 0; b < 8u; b++) {
-            const uint32_t ch = ((b < 4u ? w.x : w.y) >> (8u * (b & 3u))) & 0xffu;
-            const bool in = i + b < len;
-            if (in && s != 0xffffffffu && e == 0xffffffffu && ch == c1) e = i + b;
-            if (in && s == 0xffffffffu && ch == c0) s = i + b;
-        }
-    }
-    if (s != 0xffffffffu && e != 0xffffffffu && e - s > 1u) {
-        p += s + 1u;
-        len = e - s - 1u;
-    }
-}
-
-/* ketama_dispatch (src/hashkit/nc_ketama.c:222-246): the first point whose
- * value is >= hash, wrapping to the first point; c = {index, value} pairs */
-__device__ __forceinline__ uint32_t ketama_find(const uint32_t *c, uint32_t n, uint32_t h)
-{
-    uint32_t lo = 0, len = n;
-    while (len > 0u) {
-        const uint32_t half = len >> 1;
-        if (c[2u * (lo + half) + 1u] < h) {
-            lo += half + 1u;
-            len -= half + 1u;
-        } else {
-            len = half;
-        }
-    }
-    return c[2u * (lo == n ? 0u : lo)];
-}
-
-/* ketama_find narrowed by a 256-bucket index over the top hash byte:
- * bkt[b] = first point with value >= b << 24 (bkt[256] = n), so the answer
- * for h lies in [bkt[h >> 24], bkt[(h >> 24) + 1]] and the search takes
- * ~log2(n / 256) + 1 steps instead of log2(n) */
-__device__ __forceinline__ uint32_t ketama_find_bkt(const uint32_t *c, const uint32_t *bkt, uint32_t n, uint32_t h)
-{
-    const uint32_t b = h >> 24;
-    uint32_t lo = bkt[b], len = bkt[b + 1u] - lo;
-    while (len > 0u) {
-        const uint32_t half = len >> 1;
-        if (c[2u * (lo + half) + 1u] < h) {
-            lo += half + 1u;
-            len -= half + 1u;
-        } else {
-            len = half;
-        }
-    }
-    return c[2u * (lo == n ? 0u : lo)];
-}
-
-/* lower bound of v over the continuum values (no wrap) */
-__device__ __forceinline__ uint32_t cont_lower_bound(const uint32_t *c, uint32_t n, uint32_t v)
-{
-    uint32_t lo = 0, len = n;
-    while (len > 0u) {
-        const uint32_t half = len >> 1;
-        if (c[2u * (lo + half) + 1u] < v) {
-            lo += half + 1u;
-            len -= half + 1u;
-        } else {
-            len = half;
-        }
-    }
-    return lo;
 }
 
 constexpr uint32_t kBktBytes = 4u * 260u; /* u32[257] bucket index after an LDS-staged ketama continuum */
@@ -1619,9 +1689,18 @@ template <int DIST>
 __global__ __launch_bounds__(256) void nc_dispatch_kernel(const uint32_t *__restrict__ cont, uint32_t ncont,
                                                           uint32_t *__restrict__ io, uint64_t n)
 {
+    /* ketama: the 257-entry bucket index of the continuum (ketama_find_bkt),
+     * built once per workgroup in LDS; each lookup then searches ~log2(n/256)
+     * points of the L2-resident continuum */
+    __shared__ uint32_t bkt[DIST == kDistKetama ? 260 : 1];
+    if constexpr (DIST == kDistKetama) {
+        for (uint32_t j = threadIdx.x; j <= 256u; j += 256u)
+            bkt[j] = j == 256u ? ncont : cont_lower_bound(cont, ncont, j << 24);
+        __syncthreads();
+    }
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
         const uint32_t h = io[i];
-        io[i] = DIST == kDistKetama ? ketama_find(cont, ncont, h) : cont[2u * (h % ncont)];
+        io[i] = DIST == kDistKetama ? ketama_find_bkt(cont, bkt, ncont, h) : cont[2u * (h % ncont)];
     }
 }
 
@@ -1654,6 +1733,7 @@ struct DistArgs {
     uint32_t tag;
     int kind;
     bool wide; /* 5 KiB slab slots two tiles ahead (keys of 20+ B) instead of 3 KiB one ahead */
+    bool wg;   /* the workgroup pipeline (continuum in L2, bucket index in LDS) instead of the wave ring */
 };
 /* fused hash -> dispatch of mode MODE on the wave ring (offsets 16-byte aligned) */
 template <int MODE>
@@ -1738,11 +1818,11 @@ int num_cus()
 
 template <int MODE, bool SORT, int VAR>
 hipError_t launch_kernel(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
-                         hipStream_t stream, int var)
+                         hipStream_t stream, int var, const WrDist &dist = WrDist{nullptr, 0u, 0u})
 {
     /* persistent grid: every resident workgroup slot once (occupancy query
      * cached per instantiation), unless a cap is set */
-    void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t);
+    void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist);
     if constexpr ((VAR & 32) != 0) kern = nc_hash_kernel_rs<MODE, SORT, VAR>;
     else kern = nc_hash_kernel<MODE, SORT, VAR>;
     static int per_cu = 0;
@@ -1761,7 +1841,8 @@ hipError_t launch_kernel(const uint8_t *base, const uint64_t *off, uint64_t delt
     uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu * over;
     if (grid > ntiles) grid = ntiles;
     (void)hipGetLastError(); /* a stale error from another library's call must not be reported as ours */
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, stream, base, off, delta, nkeys, out, ntiles);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, stream, base, off, delta, nkeys, out, ntiles,
+                       dist);
     return hipGetLastError();
 }
 
@@ -1953,6 +2034,22 @@ template hipError_t nc_tu::entry<NC_TU_MODE>(const uint8_t *, const uint64_t *, 
  * ~100 servers); a larger one takes the hash-then-dispatch pair of launches,
  * the second reading the continuum through L2. */
 namespace {
+/* ketama / modula over the pre-dispatch hashes in out, in place */
+hipError_t dispatch_launch(const nc_tu::DistArgs &d, uint32_t *out, uint64_t nkeys, hipStream_t stream)
+{
+    uint64_t grid = (nkeys + 255u) / 256u;
+    const uint64_t cap = (uint64_t)num_cus() * 8u;
+    if (grid > cap) grid = cap;
+    (void)hipGetLastError();
+    if (d.kind == 0)
+        hipLaunchKernelGGL(nc_dispatch_kernel<kDistKetama>, dim3((unsigned)grid), dim3(256), 0, stream, d.cont, d.ncont,
+                           out, nkeys);
+    else
+        hipLaunchKernelGGL(nc_dispatch_kernel<kDistModula>, dim3((unsigned)grid), dim3(256), 0, stream, d.cont, d.ncont,
+                           out, nkeys);
+    return hipGetLastError();
+}
+
 /* server_pool_idx on ring shape <P, DS, DO>, four waves per workgroup */
 template <int MODE, int P, int DS, int DO>
 hipError_t dist_launch(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
@@ -1969,17 +2066,7 @@ hipError_t dist_launch(const uint8_t *base, const uint64_t *off, uint64_t delta,
     }
     hipError_t e = launch_wr<MODE, 0, P, DS, DO, kDistPre, WPW>(base, off, delta, nkeys, out, stream, wd, fixed);
     if (e != hipSuccess) return e;
-    uint64_t grid = (nkeys + 255u) / 256u;
-    const uint64_t cap = (uint64_t)num_cus() * 8u;
-    if (grid > cap) grid = cap;
-    (void)hipGetLastError();
-    if (d.kind == 0)
-        hipLaunchKernelGGL(nc_dispatch_kernel<kDistKetama>, dim3((unsigned)grid), dim3(256), 0, stream, d.cont, d.ncont,
-                           out, nkeys);
-    else
-        hipLaunchKernelGGL(nc_dispatch_kernel<kDistModula>, dim3((unsigned)grid), dim3(256), 0, stream, d.cont, d.ncont,
-                           out, nkeys);
-    return hipGetLastError();
+    return dispatch_launch(d, out, nkeys, stream);
 }
 } // namespace
 
@@ -1987,6 +2074,13 @@ template <int MODE>
 hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys,
                              uint32_t *out, hipStream_t stream, const DistArgs &d)
 {
+    if constexpr (!uses_crc_table<MODE>()) { /* the crc modes need the workgroup's LDS table slot */
+        if (d.wg) {
+            const WrDist wd{d.cont, d.ncont, d.tag};
+            return d.kind == 0 ? launch_kernel<MODE, false, 1 << 12>(base, off, delta, nkeys, out, stream, kVarOver, wd)
+                               : launch_kernel<MODE, false, 2 << 12>(base, off, delta, nkeys, out, stream, kVarOver, wd);
+        }
+    }
     return d.wide ? dist_launch<MODE, 5, 2, 3>(base, off, delta, nkeys, out, stream, d)
                   : dist_launch<MODE, 3, 1, 2>(base, off, delta, nkeys, out, stream, d);
 }
@@ -2148,7 +2242,19 @@ extern "C" rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint
     const uint8_t *base = reinterpret_cast<const uint8_t *>(kp & ~(uintptr_t)15);
     const uint64_t delta = (uint64_t)(kp & 15u);
     const bool wide = shape != nullptr && shape->key_bytes > 20u * nkeys;
-    nc_tu::DistArgs d{reinterpret_cast<const uint32_t *>(d_continuum), ncontinuum, 0u, dist, wide};
+    /* pipeline: the workgroup pipeline (continuum in L2, bucket index in LDS)
+     * for ketama pools and for any hash_tag: its eight waves per SIMD hide the
+     * search's and the tag scan's latency (C3 ketama 1.22 -> 0.71 ms, C2 with
+     * "{}" 1.56 -> 1.26, C2 ketama 0.69 -> 0.66), and for short keys (C2
+     * modula 0.56 -> 0.53); modula without a tag on 20+ B keys keeps the wave
+     * ring (one continuum read per key, ring 4-11 % ahead on C3).
+     * The crc modes always take the ring (their table has the LDS slot).
+     * Variant bit 29 forces the workgroup pipeline, bit 28 the ring (A/B). */
+    const int tuned = load_i(&g_variant);
+    bool wg = dist == NC_GPUHASH_DIST_KETAMA || hash_tag != nullptr || !wide;
+    if (tuned & (1 << 29)) wg = true;
+    if (tuned & (1 << 28)) wg = false;
+    nc_tu::DistArgs d{reinterpret_cast<const uint32_t *>(d_continuum), ncontinuum, 0u, dist, wide, wg};
     if (hash_tag != nullptr)
         d.tag = (uint32_t)(uint8_t)hash_tag[0] | ((uint32_t)(uint8_t)hash_tag[1] << 8) | (1u << 16);
     hipError_t e;
