@@ -1769,7 +1769,6 @@ constexpr int kVarRegStaged = 32;
 constexpr int kVarRingP5 = 128 | (3 << 8);
 constexpr int kVarRingP4 = 128;
 constexpr int kVarSorted = 1 << 17; /* group the tile's keys by length (the SORT pipeline) */
-constexpr int kVarRingSorted = 128 | 16384; /* 256-key wave tiles hashed in length-sorted rounds (6 KiB slots) */
 constexpr int kVarOver = 1 << 18; /* workgroup pipelines: three resident sets of workgroups per launch */
 constexpr int kVarMd5Direct = 1 << 19; /* the direct per-lane block pipeline: md5 (nc_md5_kernels.hip) and
                                           the byte-serial modes (nc_bytes_kernels.hip); options in bits 20-23 */
@@ -2115,7 +2114,6 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
     const bool crc = mode == NC_GPUHASH_CRC16 || mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A;
     const bool fnv_like = mode == NC_GPUHASH_FNV1_64 || mode == NC_GPUHASH_FNV1A_64 || mode == NC_GPUHASH_FNV1_32 ||
                           mode == NC_GPUHASH_FNV1A_32 || mode == NC_GPUHASH_HSIEH || mode == NC_GPUHASH_MURMUR;
-    const bool md5 = mode == NC_GPUHASH_MD5;
     /* the byte-serial modes of the direct pipeline (nc_bytes_kernels.hip) */
     const bool direct_bytes = crc || mode == NC_GPUHASH_ONE_AT_A_TIME || mode == NC_GPUHASH_FNV1_64 ||
                               mode == NC_GPUHASH_FNV1A_64 || mode == NC_GPUHASH_FNV1_32 || mode == NC_GPUHASH_FNV1A_32;
@@ -2135,21 +2133,17 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
     if (fixed) {
         if (mean >= 20u && mean <= 40u) { /* C3 */
             if (fnv_like) return kVarRingP5;
-            if (crc) return kVarWorkgroup | kVarOver;
-            return md5 ? (kVarRegStaged | kVarOver) : kVarRegStaged;
+            return kVarRegStaged;
         }
-        if (mean < 20u) return md5 ? (kVarWorkgroup | kVarOver) : kVarWorkgroup;
+        if (mean < 20u) return kVarWorkgroup;
         return kVarRegStaged;
     }
-    /* varying lengths: a wave runs as long as its longest key (a second md5
-     * block if any lane needs one); length-grouped tiles and oversubscribed
-     * grids rebalance that */
+    /* varying lengths: a wave runs as long as its longest key; length-grouped
+     * tiles and oversubscribed grids rebalance that */
     if (mean < 22u) { /* C2 */
-        if (md5) return kVarRingSorted;
         if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarWorkgroup | kVarSorted | kVarOver;
         return kVarWorkgroup | kVarOver;
     }
-    if (md5) return mean < 28u ? (kVarWorkgroup | kVarSorted | kVarOver) : (kVarRegStaged | kVarSorted);
     if (crc || mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarRegStaged | kVarOver;
     return kVarRegStaged;
 }
