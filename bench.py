@@ -191,12 +191,19 @@ def read_ceiling(t, rf, buf):
     rf["frac_of_read_ceiling"] = round(rf["achieved"] / probe, 4)
 
 
+PROFILED_NKEYS = {"C2": 1 << 26, "C3": 1 << 26, "C4": 1 << 25}  # tools/pmc_run.py sizes
+RUN_NKEYS = dict(PROFILED_NKEYS)  # this run's nominal keys per GPU (--nkeys / --c4-nkeys)
+
+
 def load_traffic(kernel_mode: str, workload: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this
     workload (profiles/pmc_*.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950
-    correction), or None when no such measurement exists."""
+    correction), or None when no such measurement exists or the batch is not
+    the profiled size (PROFILED_NKEYS)."""
     import glob
 
+    if PROFILED_NKEYS.get(workload) != RUN_NKEYS.get(workload):
+        return None
     best = None
     for path in sorted(glob.glob(os.path.join(HERE, "profiles", "pmc_*.json"))):
         try:
@@ -294,6 +301,7 @@ def main():
 
     spec = t.CONFIGS["C2"]["spec"]
     n_local = args.nkeys
+    RUN_NKEYS.update(C2=args.nkeys, C3=args.nkeys, C4=args.c4_nkeys)
     dev = torch.device("cuda", local)
     ceiling = md5_ceiling() if (rank == 0 and not args.no_extra) else None
 

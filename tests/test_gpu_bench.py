@@ -1,0 +1,67 @@
+"""bench.py's output contract on the device at reduced sizes: one JSON line
+with the driver's fields, the roofline and cpu_baseline objects, every
+secondary leg, and no PMC traffic borrowed from the full-size profiles."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
+
+
+@pytest.fixture(scope="module")
+def line():
+    import torch  # noqa: F401  (pages the image in before the child's own import)
+
+    cmd = [sys.executable, "-u", os.path.join(HERE, "bench.py"), "--steps", "3", "--warmup", "1",
+           "--nkeys", str(1 << 20), "--c4-nkeys", str(1 << 16), "--cpu-sample", str(1 << 16)]
+    p = subprocess.run(cmd, cwd=HERE, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rows = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(rows) == 1, p.stdout[-2000:]
+    return json.loads(rows[0])
+
+
+def test_driver_fields(line):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in line, k
+    assert line["n_gpus"] == 1 and line["steps"] == 3 and line["warmup"] == 1
+    assert line["value"] > 0 and line["ms_per_step"] > 0
+    assert line["higher_is_better"] is True and line["scaling"] == "weak"
+    assert line["dtype"] == "u8" and line["unit"] == "Mkeys/s"
+    assert "workload" in line["config"] and line["config"]["nkeys_per_gpu"] == 1 << 20
+    # value is the wall clock over the K steps: keys / (ms_per_step) within rounding
+    assert abs(line["value"] - (1 << 20) / (line["ms_per_step"] * 1e-3) / 1e6) <= 0.02 * line["value"] + 0.2
+
+
+def test_roofline(line):
+    rf = line["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert rf["achieved"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    assert rf["traffic"] is None  # the committed PMC profiles are of 2^26 keys, not 2^20
+    assert rf["alg_bytes_per_launch"] == line["config"]["key_bytes_rank0"] + 12 * (1 << 20)
+
+
+def test_cpu_baseline(line):
+    cb = line["cpu_baseline"]
+    assert "error" not in cb, cb
+    assert cb["value"] > 0 and cb["unit"] == "Mkeys/s" and cb["cores"] >= 1
+    assert cb["kind"] in ("reference", "port") and cb["sample"]
+
+
+def test_secondary_legs(line):
+    for k in ("md5", "server_idx_ketama", "c3_fnv1a_64", "c3_crc32", "c3_md5", "c4_shard",
+              "redis_key_extraction", "c5_e2e"):
+        assert k in line, k
+        assert "error" not in line[k], line[k]
+    assert line["md5"]["roofline"]["bound"] == "valu" and line["md5"]["roofline_hbm"]["bound"] == "hbm"
+    for k in ("md5", "c3_fnv1a_64", "c3_crc32", "c3_md5", "server_idx_ketama"):
+        assert line[k]["kernel_ms"] > 0
+    for mode in ("md5", "crc32", "fnv1a_64"):
+        assert line["c4_shard"][mode]["kernel_ms"] > 0
+        assert line["c4_shard"][mode]["roofline"]["traffic"] is None
