@@ -1,12 +1,17 @@
 // Compute-only md5 ceiling on gfx950: every lane runs a 61-step final block
-// on register-resident message words, no memory traffic, for three ways of
+// on register-resident message words, no memory traffic, for several ways of
 // writing a step's additions:
-//   form 0 (the kernel's, nc_md5_steps.h): a+w (VOP2), +T (VOP2 literal), +f (VOP2)
+//   form 0 (the kernel's, nc_md5_steps.h): w+T (VOP2 literal, off the step
+//          chain), v_add3(a, wT, f) (VOP3)
 //   form 1: hipcc's default: a+w (VOP2), s_mov T, v_add3(., f, sT) (VOP3)
-//   form 2: v_add3(a, w, f) (VOP3), +T (VOP2 literal)
-// Prints ns per 64-lane round per SIMD and the implied C3 time (2^20 rounds
-// over 1024 SIMDs).
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -Itwemproxy_amd/csrc -Iinclude tools/probes/md5_rate.hip -o tools/probes/md5_rate
+//   form 2 (the round-2 kernel's): v_add3(a, w, f) (VOP3), +T (VOP2 literal)
+//   form 3: form 0 written out here (a check of the header's form)
+//   form 4: T in 64 SGPRs set before the loop, v_add3(a, w, sT), +f (VOP2)
+//   form 5: form 2's ops, the 61 steps as one inline-asm statement
+//           (md5_asm.inc, tools/gen_md5_asm.py): no hazard s_nops
+// Prints a check of form 5 against form 0, then ns per 64-lane round per SIMD
+// and the implied C3 time (2^20 rounds over 1024 SIMDs). Built by
+// twemproxy_amd/csrc/Makefile (target all).
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
@@ -15,8 +20,33 @@
 
 using namespace nc_md5s;
 
+/* Steps 0..60 / 61..63 as ONE inline-asm statement each (nc_md5_asm.inc,
+ * tools/gen_md5_asm.py): the same five VALU ops per step as md5_step, without
+ * the s_nop hipcc's hazard recognizer puts after every inline-asm def
+ * (measured slower than the kernel's form: the steps can no longer
+ * interleave with hipcc's scheduling). */
+#include "md5_asm.inc"
+
+#define NC_MD5_ASM_OPERANDS(v, w, t)                                                                        \
+    : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "=&v"(t)                                           \
+    : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]), "v"(w[8]), \
+      "v"(w[9]), "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15])
+
+__device__ __forceinline__ void md5_steps_asm_0_61(uint32_t (&v)[4], const uint32_t (&w)[16])
+{
+    uint32_t t; /* scratch */
+    asm(NC_MD5_ASM_STEPS_0_61 NC_MD5_ASM_OPERANDS(v, w, t));
+}
+
+__device__ __forceinline__ void md5_steps_asm_61_64(uint32_t (&v)[4], const uint32_t (&w)[16])
+{
+    uint32_t t;
+    asm(NC_MD5_ASM_STEPS_61_64 NC_MD5_ASM_OPERANDS(v, w, t));
+}
+
+
 template <int FORM, int I>
-__device__ __forceinline__ void step(uint32_t (&v)[4], const uint32_t (&w)[16])
+__device__ __forceinline__ void step(uint32_t (&v)[4], const uint32_t (&w)[16], const uint32_t (&sT)[64])
 {
     if constexpr (FORM == 0) {
         md5_step<I>(v, w);
@@ -31,6 +61,14 @@ __device__ __forceinline__ void step(uint32_t (&v)[4], const uint32_t (&w)[16])
         uint32_t a;
         if constexpr (FORM == 1) {
             a = v[u] + w[kM[I]] + kT[I] + f;
+        } else if constexpr (FORM == 3) {
+            uint32_t wt = w[kM[I]] + kT[I];
+            asm("" : "+v"(wt));
+            a = v[u] + wt + f;
+        } else if constexpr (FORM == 4) {
+            uint32_t x;
+            asm("v_add3_u32 %0, %1, %2, %3" : "=v"(x) : "v"(v[u]), "v"(w[kM[I]]), "s"(sT[I]));
+            a = x + f;
         } else {
             uint32_t x;
             asm("v_add3_u32 %0, %1, %2, %3" : "=v"(x) : "v"(v[u]), "v"(w[kM[I]]), "v"(f));
@@ -41,9 +79,10 @@ __device__ __forceinline__ void step(uint32_t (&v)[4], const uint32_t (&w)[16])
 }
 
 template <int FORM, int... I>
-__device__ __forceinline__ void steps(uint32_t (&v)[4], const uint32_t (&w)[16], std::integer_sequence<int, I...>)
+__device__ __forceinline__ void steps(uint32_t (&v)[4], const uint32_t (&w)[16], const uint32_t (&sT)[64],
+                                      std::integer_sequence<int, I...>)
 {
-    (step<FORM, I>(v, w), ...);
+    (step<FORM, I>(v, w, sT), ...);
 }
 
 template <int FORM>
@@ -53,9 +92,15 @@ __global__ __launch_bounds__(256) void md5_rounds(unsigned *out, int rounds)
 #pragma unroll
     for (int t = 0; t < 16; t++) w[t] = threadIdx.x * 0x9e3779b9u + t;
     uint32_t acc = 0;
+    uint32_t sT[64];
+    if constexpr (FORM == 4) {
+#pragma unroll
+        for (int i = 0; i < 64; i++) asm volatile("s_mov_b32 %0, %1" : "=s"(sT[i]) : "i"(kT[i]));
+    }
     for (int r = 0; r < rounds; r++) {
         uint32_t v[4] = {0x67452301u + acc, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-        steps<FORM>(v, w, std::make_integer_sequence<int, 61>{});
+        if constexpr (FORM == 5) md5_steps_asm_0_61(v, w);
+        else steps<FORM>(v, w, sT, std::make_integer_sequence<int, 61>{});
         acc += v[0];
         w[r & 15] ^= acc; /* keeps the rounds dependent on each other's data */
     }
@@ -83,16 +128,46 @@ static void run(int wps, unsigned *o, int cus)
            FORM, wps, ms, ns_per_round, ns_per_round * 1024 * 1e-6);
 }
 
+template <int FORM>
+__global__ void md5_check(unsigned *out)
+{
+    uint32_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) w[t] = (threadIdx.x + 1u) * 0x9e3779b9u ^ (t * 0x85ebca6bu);
+    uint32_t v[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    if constexpr (FORM == 5) {
+        md5_steps_asm_0_61(v, w);
+        md5_steps_asm_61_64(v, w);
+    } else {
+        md5_steps(v, w, std::make_integer_sequence<int, 61>{});
+        md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
+    }
+    for (int i = 0; i < 4; i++) out[threadIdx.x * 4 + i] = v[i];
+}
+
 int main()
 {
     hipDeviceProp_t p;
     (void)hipGetDeviceProperties(&p, 0);
     unsigned *o;
     (void)hipMalloc(&o, 1 << 20);
+    {
+        unsigned h0[256], h5[256];
+        hipLaunchKernelGGL(md5_check<0>, dim3(1), dim3(64), 0, 0, o);
+        (void)hipMemcpy(h0, o, sizeof h0, hipMemcpyDeviceToHost);
+        hipLaunchKernelGGL(md5_check<5>, dim3(1), dim3(64), 0, 0, o);
+        (void)hipMemcpy(h5, o, sizeof h5, hipMemcpyDeviceToHost);
+        int bad = 0;
+        for (int i = 0; i < 256; i++) bad += h0[i] != h5[i];
+        printf("{\"asm_steps_match\": %s, \"mismatches\": %d}\n", bad ? "false" : "true", bad);
+    }
     for (int wps : {4, 8}) {
         run<0>(wps, o, p.multiProcessorCount);
         run<1>(wps, o, p.multiProcessorCount);
         run<2>(wps, o, p.multiProcessorCount);
+        run<3>(wps, o, p.multiProcessorCount);
+        run<4>(wps, o, p.multiProcessorCount);
+        run<5>(wps, o, p.multiProcessorCount);
     }
     return 0;
 }

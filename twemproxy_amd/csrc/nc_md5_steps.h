@@ -34,14 +34,15 @@ __device__ __forceinline__ void md5_step(uint32_t (&v)[4], const uint32_t (&w)[1
     else if constexpr (I < 32) f = NC_MD5_G(b, c, d);
     else if constexpr (I < 48) f = NC_MD5_H(b, c, d);
     else f = NC_MD5_I(b, c, d);
-    /* a + w + f by one v_add3_u32, then + T by a VOP2 literal add: five VALU
-     * instructions per step and no scalar s_mov of T (hipcc's default form,
-     * a+w, s_mov T, v_add3, is 5 % slower; three VOP2 adds 15 % slower:
-     * tools/probes/md5_rate.hip) */
-    uint32_t x = v[u] + w[kM[I]] + f;
-    asm("" : "+v"(x)); /* keeps T out of the sum: hipcc would reassociate it into an s_mov + v_add3 */
-    const uint32_t a = x + kT[I];
-    v[u] = nc_rotl(a, kS[I]) + b;
+    /* w + T by a VOP2 literal add off the step's dependency chain, then
+     * a + (w + T) + f by one v_add3_u32: five VALU instructions per step, no
+     * scalar s_mov of T, and a four-op chain f -> add3 -> rotate -> add
+     * (tools/probes/md5_rate.hip form 3: 13 % faster than a + w + f, + T at 4
+     * waves per SIMD, 1 % at 8; hipcc's default form, a + w, s_mov T, v_add3,
+     * is slower than both) */
+    uint32_t wt = w[kM[I]] + kT[I];
+    asm("" : "+v"(wt)); /* keeps T out of the sum: hipcc would reassociate it into an s_mov + v_add3 */
+    v[u] = nc_rotl(v[u] + wt + f, kS[I]) + b;
 }
 
 template <int... I>
