@@ -134,12 +134,13 @@ def test_auto_policy_choices():
     """Shape-driven pipeline choice (host logic): md5 always on
     the direct per-lane block pipeline (its LDS-DMA line image from 64-byte
     keys); the byte-serial modes on the direct pipeline for long keys and the
-    crcs for fixed short keys; the register-staged workgroup pipeline when the
+    crcs for fixed short keys (tiles interleaved over the grid, 32 per wave,
+    for both); the register-staged workgroup pipeline when the
     shape is unknown; oversubscribed workgroup grids (and length grouping) for
     varying lengths; the wave ring for fixed 20-40 B fnv-like keys."""
     WG, RS, RING5, RING4 = 1 << 16, 32, 128 | (3 << 8), 128
     SORTED, OVER = 1 << 17, 1 << 18
-    DIRECT, DIRECT_LDS = 1 << 19, 4 << 20
+    DIRECT, DIRECT_LDS, IL32 = 1 << 19, 4 << 20, (8 | 2) << 20
     n = 1 << 26
     assert t.pick_variant("fnv1a_64", n) == RS
     assert t.pick_variant("md5", n) == DIRECT  # unknown shape
@@ -156,7 +157,7 @@ def test_auto_policy_choices():
     for name in ("fnv1_64", "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == RING5, name
     for name in ("crc16", "crc32", "crc32a"):
-        assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT, name
+        assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT | IL32, name
     for name in ("one_at_a_time", "jenkins"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == RS, name
     assert t.pick_variant("md5", n, (32 * n, 32, 32)) == DIRECT
@@ -164,7 +165,7 @@ def test_auto_policy_choices():
     assert t.pick_variant("fnv1a_64", n, (8 * n, 8, 8)) == WG
     assert t.pick_variant("md5", n, (16 * n, 16, 16)) == DIRECT
     for name in ("crc32", "fnv1a_64", "one_at_a_time", "crc16", "fnv1_32"):
-        assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS, name
+        assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | IL32, name
     assert t.pick_variant("md5", n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS
     assert t.pick_variant("md5", n >> 3, (128 * (n >> 3), 128, 128)) == DIRECT | DIRECT_LDS
     assert t.pick_variant("murmur", n >> 3, (256 * (n >> 3), 256, 256)) == RING4

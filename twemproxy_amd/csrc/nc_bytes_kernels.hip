@@ -6,15 +6,17 @@
  * from registers (fixed-length keys: every lane of a wave runs the same byte
  * count) or, for long keys, from the LDS-DMA block image.
  *
- * The crc table lookup is the crc modes' bottleneck on the other pipelines:
- * one 1 KiB table, a random entry per lane (~3.5-way bank conflicts) and a
- * dependent lookup per byte. Here whole words go through slicing-by-4 tables
- * (four independent lookups) replicated over 8 bank groups (see look()).
+ * The crc table lookup is the crc modes' bottleneck on the byte-table
+ * pipelines: one 1 KiB table, a random entry per lane (~3.5-way bank
+ * conflicts) and a dependent lookup per byte. Here whole words go through
+ * slicing-by-4 tables (four independent lookups) replicated over 8 bank
+ * groups (nc_crc_slice.h).
  */
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
 
+#include "nc_crc_slice.h"
 #include "nc_direct.h"
 #include "nc_gpuhash.h"
 #include "nc_hash_algo.h"
@@ -49,46 +51,17 @@ __device__ __forceinline__ uint32_t final_state(uint32_t h)
     return h;
 }
 
-/* ---- crc tables: slicing-by-4, replicated over 8 bank groups ----
- * Four tables T0..T3 of 256 entries: T0 is the byte table
- * (src/hashkit/nc_crc16.c:20-53, nc_crc32.c:27-92, generated from the
- * polynomials), Tk advances Tk-1 by one more zero byte, so a whole word costs
- * four INDEPENDENT lookups (one LDS latency) instead of four chained ones.
- * Each entry is stored 8 times, copy c for lanes with (lane & 7) == c: lanes
- * of one copy class meet only when their entries agree mod 4, which keeps a
- * 64-lane lookup near conflict-free. Word of (table k, entry e, copy c):
- * (k * 256 + e) * 8 + c. 32 KiB. */
+/* ---- crc tables: slicing-by-4 (nc_crc_slice.h), replicated over 8 bank
+ * groups (R = 8, 32 KiB) ---- */
 constexpr uint32_t kCopies = 8;
-constexpr uint32_t kTabWords = 4u * 256u * kCopies;
+constexpr uint32_t kTabWords = nc_slice::table_words<kCopies>();
 
-template <int MODE>
-__device__ __forceinline__ uint32_t tab_entry(uint32_t k, uint32_t e)
-{
-    if constexpr (MODE == NC_GPUHASH_CRC16) { /* Tk[e] = e * x^(16 + 8k) mod P, 16 bits */
-        uint32_t v = nc_crc16_entry(e);
-        for (uint32_t j = 0; j < k; j++) v = ((v << 8) ^ nc_crc16_entry(v >> 8)) & 0xffffu;
-        return v;
-    } else { /* reflected: Tk[e] = (Tk-1[e] >> 8) ^ T0[Tk-1[e] & 0xff] */
-        uint32_t v = nc_crc32_entry(e);
-        for (uint32_t j = 0; j < k; j++) v = (v >> 8) ^ nc_crc32_entry(v & 0xffu);
-        return v;
-    }
-}
-
-/* table k, entry idx (0..255), in this lane's copy: byte address ((k*256 + idx) << 5) | lc4 */
-__device__ __forceinline__ uint32_t look(const uint32_t *tab, uint32_t idx, uint32_t lc4, uint32_t k = 0)
-{
-    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(tab) + (k << 13) + ((idx << 5) | lc4));
-}
-
-/* byte j (0..3) of word w into state h */
+/* byte j (0..3) of word w into state h (the crcs through T0) */
 template <int MODE>
 __device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t w, int j, const uint32_t *tab, uint32_t lane4)
 {
     const uint32_t b = (w >> (8 * j)) & 0xffu;
-    if constexpr (MODE == NC_GPUHASH_CRC16) return NC_CRC16_NEXT(h, look(tab, NC_CRC16_IDX(h, b), lane4));
-    else if constexpr (MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A)
-        return NC_CRC32_NEXT(h, look(tab, NC_CRC32_IDX(h, b), lane4));
+    if constexpr (has_table<MODE>()) return nc_slice::byte<MODE, kCopies>(h, b, tab, lane4);
     else if constexpr (MODE == NC_GPUHASH_FNV1A_64) return nc_fnv1a_64_step(h, b);
     else if constexpr (MODE == NC_GPUHASH_FNV1_64) return nc_fnv1_64_step(h, b);
     else if constexpr (MODE == NC_GPUHASH_FNV1_32) return nc_fnv1_32_step(h, b);
@@ -100,20 +73,8 @@ __device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t w, int j, con
 template <int MODE>
 __device__ __forceinline__ uint32_t word_step(uint32_t h, uint32_t w, const uint32_t *tab, uint32_t lc4)
 {
-    if constexpr (MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A) {
-        /* reflected slicing-by-4: the word meets the state's low bytes */
-        const uint32_t x = h ^ w;
-        return look(tab, x >> 24, lc4, 0) ^ look(tab, (x >> 16) & 0xffu, lc4, 1) ^ look(tab, (x >> 8) & 0xffu, lc4, 2) ^
-               look(tab, x & 0xffu, lc4, 3);
-    } else if constexpr (MODE == NC_GPUHASH_CRC16) {
-        /* MSB-first slicing-by-4 on the 16-bit crc: V = crc << 16 ^ the word's
-         * bytes big-endian; crc' = V * x^16 mod P. The unmasked 32-bit state
-         * (nc_crc16.c:59-65) keeps shifted history in bits 16-31; those are
-         * rebuilt by the byte steps at the key's end (block_step leaves the last
-         * 2+ bytes to them), so here only the low 16 bits are carried. */
-        const uint32_t v = ((h & 0xffffu) << 16) ^ __builtin_bswap32(w);
-        return look(tab, v >> 24, lc4, 3) ^ look(tab, (v >> 16) & 0xffu, lc4, 2) ^ look(tab, (v >> 8) & 0xffu, lc4, 1) ^
-               look(tab, v & 0xffu, lc4, 0);
+    if constexpr (has_table<MODE>()) {
+        return nc_slice::word<MODE, kCopies>(h, w, tab, lc4);
     } else {
 #pragma unroll
         for (int j = 0; j < 4; j++) h = byte_step<MODE>(h, w, j, tab, lc4);
@@ -141,8 +102,8 @@ __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], 
         const int32_t kb = nb - 4 * t;
         const uint32_t w = d[t >> 2][t & 3];
         /* crc16 keeps its key's last 2+ bytes for the byte steps, which
-         * rebuild the state's history bits (see word_step) */
-        constexpr int32_t kWhole = MODE == NC_GPUHASH_CRC16 ? 6 : 4;
+         * rebuild the state's history bits (nc_crc_slice.h word) */
+        constexpr int32_t kWhole = nc_slice::whole<MODE>();
         if (kb >= kWhole) h = word_step<MODE>(h, w, tab, lane4);
         else if (kb > 0) h = bytes_step<MODE>(h, w, kb, tab, lane4);
     }
@@ -161,7 +122,7 @@ template <int MODE, bool LDS>
 __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__restrict__ keys,
                                                               const uint64_t *__restrict__ off, uint64_t nkeys,
                                                               uint32_t *__restrict__ out, uint64_t ntiles,
-                                                              uint32_t chunk)
+                                                              uint32_t chunk, bool interleave)
 {
     /* a round consumes RB bytes of every key: one 64-byte block from
      * registers, or (LDS) one 128-byte line from the image */
@@ -169,21 +130,18 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
     __shared__ uint32_t tab[has_table<MODE>() ? kTabWords : 1];
     __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kLineImage : 16];
     if constexpr (has_table<MODE>()) {
-        for (uint32_t i = threadIdx.x; i < 4u * 256u; i += 1024u) {
-            const uint32_t v = tab_entry<MODE>(i >> 8, i & 255u);
-#pragma unroll
-            for (uint32_t c = 0; c < kCopies; c++) tab[i * kCopies + c] = v;
-        }
+        nc_slice::fill<MODE, kCopies>(tab, threadIdx.x, 1024u);
         __syncthreads();
     }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane4 = (lane & (kCopies - 1u)) * 4u; /* this lane's table copy */
-    uint64_t tile = ((uint64_t)blockIdx.x * kWaves + wave) * chunk;
-    const uint64_t tlast = ntiles < tile + chunk ? ntiles : tile + chunk;
+    const uint32_t lane4 = nc_slice::copy_of<kCopies>(lane); /* this lane's table copy */
+    const Tiles tiles = wave_tiles(ntiles, chunk, kWaves, wave, interleave);
+    uint64_t tile = 0; /* local tile index */
+    const uint64_t tlast = tiles.n;
     if (tile >= tlast) return;
     Walker wk;
-    wk.init(keys, off, nkeys, tlast, lane);
+    wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + (LDS ? wave * kLineImage : 0u);
 
     TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
@@ -217,7 +175,7 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
                 if (rem > 64) h = block_step<MODE>(h, nxt, rem - 64, tab, lane4);
             }
             if (rem <= (int32_t)RB) {
-                const rsrc_t rout = make_rsrc(out + tile * 64u, 256u);
+                const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
                 __builtin_amdgcn_raw_buffer_store_b32(final_state<MODE>(h), rout, (int)(lane * 4u), 0, kAuxNt);
             }
         }
@@ -257,15 +215,16 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
     (void)hipGetLastError();
     if (var & 4)
         hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true>), dim3((unsigned)grid), dim3(1024), 0, stream, d_keys,
-                           d_off, nkeys, d_out, ntiles, chunk);
+                           d_off, nkeys, d_out, ntiles, chunk, (var & 8) != 0);
     else
         hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false>), dim3((unsigned)grid), dim3(1024), 0, stream, d_keys,
-                           d_off, nkeys, d_out, ntiles, chunk);
+                           d_off, nkeys, d_out, ntiles, chunk, (var & 8) != 0);
     return hipGetLastError();
 }
 
 /* the byte-serial modes on the direct pipeline; var: bits 0-1 tiles per wave
- * (16, 8, 32, 64), bit 2 the LDS-DMA block image (long keys). nkeys < 2^32. */
+ * (16, 8, 32, 64), bit 2 the LDS-DMA block image (long keys), bit 3 a wave's
+ * tiles interleaved over the grid (else consecutive). nkeys < 2^32. */
 bool supports(int mode)
 {
     switch (mode) {

@@ -1774,6 +1774,8 @@ constexpr int kVarMd5Direct = 1 << 19; /* the direct per-lane block pipeline: md
                                           the byte-serial modes (nc_bytes_kernels.hip); options in bits 20-23 */
 constexpr int kVarDirect = kVarMd5Direct;
 constexpr int kVarDirectLds = 4 << 20; /* its LDS-DMA block image (long keys) */
+constexpr int kVarDirectIl32 = (8 | 2) << 20; /* a wave's tiles interleaved over the grid, 32 per wave (nc_direct.h
+                                                 wave_tiles) */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2122,14 +2124,14 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
          * crc32 3.56 -> 2.24 ms, fnv1a_64 3.06 -> 2.15, one_at_a_time 3.22 ->
          * 2.48; 128-byte keys 0.79 -> 0.62 ms); the word modes keep the wave
          * ring, deeper or wider slab slots */
-        if (direct_bytes) return kVarDirect | kVarDirectLds;
+        if (direct_bytes) return kVarDirect | kVarDirectLds | kVarDirectIl32; /* interleaved: C4 shard 1.92 -> 1.84 ms (crc32), 1.75 -> 1.66 (fnv1a_64) */
         if (mode == NC_GPUHASH_HSIEH) return kVarRingP5;
         return kVarRingP4;
     }
     /* fixed-length short keys: the crcs' slicing-by-4 tables on the direct
      * pipeline (C3: 0.70 -> 0.61 ms); varying lengths keep the length-grouped
      * workgroup pipelines (a direct wave runs to its longest key) */
-    if (crc && fixed && mean <= 64u) return kVarDirect;
+    if (crc && fixed && mean <= 64u) return kVarDirect | kVarDirectIl32; /* interleaved: C3 crc32 0.62 -> 0.575 ms */
     if (fixed) {
         if (mean >= 20u && mean <= 40u) { /* C3 */
             if (fnv_like) return kVarRingP5;

@@ -151,7 +151,8 @@ __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__re
 template <bool LDS>
 __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
-                                                           uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
+                                                           uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk,
+                                                           bool interleave)
 {
     __shared__ uint32_t qmem[kWaves * kQWords * kQ];
     /* LDS: the next round's blocks arrive by LDS-DMA into a per-wave 4 KiB
@@ -162,12 +163,13 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
     /* a wave owns `chunk` consecutive tiles; the grid covers every tile once
      * and the hardware dispatcher balances the waves (no persistent grid to
      * size from an occupancy estimate) */
-    uint64_t tile = ((uint64_t)blockIdx.x * kWaves + wave) * chunk;
-    const uint64_t tlast = ntiles < tile + chunk ? ntiles : tile + chunk;
+    const Tiles tiles = wave_tiles(ntiles, chunk, kWaves, wave, interleave);
+    uint64_t tile = 0; /* local tile index */
+    const uint64_t tlast = tiles.n;
     if (tile >= tlast) return;
     Queue q{qmem + wave * kQWords * kQ, 0u, 0u};
     Walker wk;
-    wk.init(keys, off, nkeys, tlast, lane);
+    wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + (LDS ? wave * kImage : 0u);
     auto load_blk = [&](const TileKeys &t, uint32_t b, u32x4 (&d)[4]) __attribute__((always_inline)) {
         if constexpr (LDS) wk.dma(t, b, img);
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
             uint32_t v[4] = {st[0], st[1], st[2], st[3]};
             md5_steps(v, w, std::make_integer_sequence<int, 61>{});
             if (fin) {
-                const rsrc_t rout = make_rsrc(out + tile * 64u, 256u);
+                const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
                 __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
             } else {
                 md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
@@ -243,7 +245,7 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
                 q.w[2 * kQ + slot] = st[2];
                 q.w[3 * kQ + slot] = st[3];
                 q.w[4 * kQ + slot] = len;
-                q.w[5 * kQ + slot] = (uint32_t)(tile * 64u + lane);
+                q.w[5 * kQ + slot] = (uint32_t)(wk.key0(tile) + lane);
             }
             q.count += (uint32_t)__builtin_popcountll(tm);
             if (q.count >= 64u) run_tail(q, lane, out);
@@ -276,16 +278,18 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
  */
 __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
-                                                           uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
+                                                           uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk,
+                                                           bool interleave)
 {
     __shared__ __attribute__((aligned(16))) uint8_t kbuf[kWaves * kLineImage];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint64_t tile = ((uint64_t)blockIdx.x * kWaves + wave) * chunk;
-    const uint64_t tlast = ntiles < tile + chunk ? ntiles : tile + chunk;
+    const Tiles tiles = wave_tiles(ntiles, chunk, kWaves, wave, interleave);
+    uint64_t tile = 0; /* local tile index */
+    const uint64_t tlast = tiles.n;
     if (tile >= tlast) return;
     Walker wk;
-    wk.init(keys, off, nkeys, tlast, lane);
+    wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + wave * kLineImage;
     TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
     Offs no = wk.load_off(tile + 1u);
@@ -307,7 +311,7 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
         uint32_t v[4] = {st[0], st[1], st[2], st[3]};
         md5_steps(v, w, std::make_integer_sequence<int, 61>{});
         if (fin) {
-            const rsrc_t rout = make_rsrc(out + tile * 64u, 256u);
+            const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
             __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
         } else {
             md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
@@ -338,7 +342,7 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
             w[0] = (cur_t.len & 63u) == 0u ? 0x80u : 0u;
             w[14] = cur_t.len << 3;
             w[15] = cur_t.len >> 29;
-            const rsrc_t rout = make_rsrc(out + tile * 64u, 256u);
+            const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
             __builtin_amdgcn_raw_buffer_store_b32(md5_block_final_a(st, w), rout, (int)(lane * 4u), 0, kAuxNt);
         }
         if (more) {
@@ -372,10 +376,10 @@ hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, 
     (void)hipGetLastError();
     if (var & 4)
         hipLaunchKernelGGL(nc_md5_lines_kernel, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off, nkeys, d_out,
-                           ntiles, chunk);
+                           ntiles, chunk, (var & 8) != 0);
     else
         hipLaunchKernelGGL(nc_md5_direct_kernel<false>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off,
-                           nkeys, d_out, ntiles, chunk);
+                           nkeys, d_out, ntiles, chunk, (var & 8) != 0);
     return hipGetLastError();
 }
 
