@@ -9,7 +9,8 @@ the shape policy; others are nc_gpuhash_set_tuning variant bits. For every
 (config, mode) the outputs of each variant are compared with the first
 variant's, key for key, and 512 sampled keys with the per-key host symbols.
 Prints one JSON line per (config, mode, variant): median / min kernel ms
-(hipEvents), Gkeys/s and the algorithmic HBM fraction.
+(hipEvents), Gkeys/s and the algorithmic HBM fraction. --lib times another
+build of the library (e.g. an older commit's) in this process.
 """
 import argparse
 import json
@@ -41,13 +42,17 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--nkeys", type=int, default=1 << 26)
+    ap.add_argument("--lib", default="", help="another build of libnc_gpuhash.so (same-box A/B of builds)")
     args = ap.parse_args()
 
     import numpy as np
     import torch
 
-    import twemproxy_amd as t
     from twemproxy_amd import _lib as L
+
+    if args.lib:
+        L.LIB_PATH = os.path.abspath(args.lib)
+    import twemproxy_amd as t
 
     variants = [int(v) for v in args.variants.split(",")]
     rng = np.random.default_rng(1)
@@ -88,7 +93,7 @@ def main():
             for v in variants:
                 med = statistics.median(res[v])
                 alg = kb + 12.0 * n
-                print(json.dumps({"config": cfg, "mode": mode, "var": v, "nkeys": n, "key_bytes": kb,
+                print(json.dumps({"lib": os.path.basename(L.LIB_PATH), "config": cfg, "mode": mode, "var": v, "nkeys": n, "key_bytes": kb,
                                   "ms_median": round(med, 4), "ms_min": round(min(res[v]), 4),
                                   "gkeys_s": round(n / med / 1e6, 2), "hbm_frac": round(alg / med / 1e6 / 8000.0, 4),
                                   "check": ok[v]}), flush=True)

@@ -118,11 +118,11 @@ __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], 
  * key that has one into its state; the next round's block is in flight (the
  * other register set, or the LDS image) while this one computes.
  */
-template <int MODE, bool LDS>
+template <int MODE, bool LDS, bool IL>
 __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__restrict__ keys,
                                                               const uint64_t *__restrict__ off, uint64_t nkeys,
                                                               uint32_t *__restrict__ out, uint64_t ntiles,
-                                                              uint32_t chunk, bool interleave)
+                                                              uint32_t chunk)
 {
     /* a round consumes RB bytes of every key: one 64-byte block from
      * registers, or (LDS) one 128-byte line from the image */
@@ -136,11 +136,11 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane4 = nc_slice::copy_of<kCopies>(lane); /* this lane's table copy */
-    const Tiles tiles = wave_tiles(ntiles, chunk, kWaves, wave, interleave);
+    const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
     uint64_t tile = 0; /* local tile index */
     const uint64_t tlast = tiles.n;
     if (tile >= tlast) return;
-    Walker wk;
+    Walker<IL> wk;
     wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + (LDS ? wave * kLineImage : 0u);
 
@@ -213,12 +213,21 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
     const uint64_t grid = (ntiles + (uint64_t)kWaves * chunk - 1u) / ((uint64_t)kWaves * chunk);
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     (void)hipGetLastError();
-    if (var & 4)
-        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true>), dim3((unsigned)grid), dim3(1024), 0, stream, d_keys,
-                           d_off, nkeys, d_out, ntiles, chunk, (var & 8) != 0);
-    else
-        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false>), dim3((unsigned)grid), dim3(1024), 0, stream, d_keys,
-                           d_off, nkeys, d_out, ntiles, chunk, (var & 8) != 0);
+    const bool il = (var & 8) != 0;
+    if (var & 4) {
+        if (il)
+            hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true>), dim3((unsigned)grid), dim3(1024), 0, stream,
+                               d_keys, d_off, nkeys, d_out, ntiles, chunk);
+        else
+            hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, false>), dim3((unsigned)grid), dim3(1024), 0, stream,
+                               d_keys, d_off, nkeys, d_out, ntiles, chunk);
+    } else if (il) {
+        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false, true>), dim3((unsigned)grid), dim3(1024), 0, stream,
+                           d_keys, d_off, nkeys, d_out, ntiles, chunk);
+    } else {
+        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false, false>), dim3((unsigned)grid), dim3(1024), 0, stream,
+                           d_keys, d_off, nkeys, d_out, ntiles, chunk);
+    }
     return hipGetLastError();
 }
 

@@ -52,33 +52,28 @@ struct TileKeys {
 
 /* Offsets of a tile, as loaded (consumed one round later). */
 struct Offs {
-    uint32_t s;   /* low dword of this lane's key start */
-    uint32_t e63; /* wave-uniform: low dword of the tile's end, off[min(k0 + 64, nkeys)] */
+    uint32_t s, e; /* low dwords of this lane's key start and end */
     uint64_t s0;
 };
 
-/* lane i <- lane i + 1 (DPP wave_shl:1); lane 63 keeps `old` */
-__device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t old)
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x130, 0xf, 0xf, false);
-}
-
 /* A wave's tiles: local index j = 0 .. n-1 is global tile base + j * S.
- * Consecutive (S = 1: `chunk` neighbouring tiles per wave) or interleaved over
- * the grid (S = every wave of the launch), in which case the resident waves
- * read neighbouring tiles at any moment instead of regions `chunk` tiles
- * apart. Either way the grid covers every tile once. */
+ * Consecutive (IL false, S = 1: `chunk` neighbouring tiles per wave) or
+ * interleaved over the grid (IL, S = every wave of the launch), in which case
+ * the resident waves read neighbouring tiles at any moment instead of regions
+ * `chunk` tiles apart. Either way the grid covers every tile once. */
+template <bool IL>
 struct Tiles {
     uint64_t base, S, n;
-    __device__ __forceinline__ uint64_t at(uint64_t j) const { return base + j * S; }
+    __device__ __forceinline__ uint64_t at(uint64_t j) const { return IL ? base + j * S : base + j; }
 };
 
-__device__ __forceinline__ Tiles wave_tiles(uint64_t ntiles, uint32_t chunk, uint32_t waves_per_block, uint32_t wave,
-                                            bool interleave)
+template <bool IL>
+__device__ __forceinline__ Tiles<IL> wave_tiles(uint64_t ntiles, uint32_t chunk, uint32_t waves_per_block,
+                                                uint32_t wave)
 {
     const uint64_t w = (uint64_t)blockIdx.x * waves_per_block + wave;
-    Tiles t;
-    if (interleave) {
+    Tiles<IL> t;
+    if constexpr (IL) {
         t.base = w;
         t.S = (uint64_t)gridDim.x * waves_per_block;
         t.n = w < ntiles ? (ntiles - w + t.S - 1u) / t.S : 0u;
@@ -91,16 +86,18 @@ __device__ __forceinline__ Tiles wave_tiles(uint64_t ntiles, uint32_t chunk, uin
     return t;
 }
 
+template <bool IL>
 struct Walker {
     const uint8_t *keys;
     const uint64_t *off;
     uint64_t nkeys;
     uint64_t kbytes; /* readable bytes from keys: off[nkeys] + NC_GPUHASH_PAD */
-    Tiles tiles;     /* this wave's tiles; local indices below */
+    Tiles<IL> tiles; /* this wave's tiles; local indices below */
     uint64_t tlast;  /* = tiles.n */
     uint32_t lane;
 
-    __device__ __forceinline__ void init(const uint8_t *k, const uint64_t *o, uint64_t n, const Tiles &tl, uint32_t ln)
+    __device__ __forceinline__ void init(const uint8_t *k, const uint64_t *o, uint64_t n, const Tiles<IL> &tl,
+                                         uint32_t ln)
     {
         keys = k;
         off = o;
@@ -115,17 +112,18 @@ struct Walker {
     __device__ __forceinline__ uint64_t key0(uint64_t tl) const { return tiles.at(tl) * 64u; }
 
     /* offsets of local tile tl; this wave's last tile again past its range, so
-     * that every round issues the same loads (keys past nkeys read as 0). One
-     * vector load per lane (its key's start); a key's end is the next lane's
-     * start (keys_of), the tile's last end comes by a scalar load. */
+     * that every round issues the same loads (keys past nkeys read as 0).
+     * (Measured: taking a key's end from the next lane by DPP, or the tile
+     * base by vector load + v_readlane, costs md5 1.5 % each and gains the
+     * crcs nothing.) */
     __device__ __forceinline__ Offs load_off(uint64_t tl) const
     {
         const uint64_t k0 = key0(tl < tlast ? tl : tlast - 1u);
         const rsrc_t r = make_rsrc(off + k0, (nkeys + 1u - k0) * 8u);
         Offs o;
         o.s = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u), 0, kAuxNt);
+        o.e = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u + 8u), 0, kAuxNt);
         o.s0 = off[k0];
-        o.e63 = reinterpret_cast<const uint32_t *>(off + (k0 + 64u < nkeys ? k0 + 64u : nkeys))[0];
         return o;
     }
 
@@ -134,8 +132,8 @@ struct Walker {
         TileKeys t;
         t.s0 = o.s0;
         t.srel = o.s - (uint32_t)o.s0;
-        t.len = from_next_lane(o.s, o.e63) - o.s;
-        t.valid = tl < tlast && key0(tl) + lane < nkeys;
+        t.len = o.e - o.s;
+        t.valid = key0(tl) + lane < nkeys;
         return t;
     }
 

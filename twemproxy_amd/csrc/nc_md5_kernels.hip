@@ -148,11 +148,10 @@ __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__re
  * key i = keys[off[i], off[i+1]); keys stays readable NC_GPUHASH_PAD bytes
  * past off[nkeys]. A tile of 64 keys spans less than 4 GiB.
  */
-template <bool LDS>
+template <bool LDS, bool IL>
 __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
-                                                           uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk,
-                                                           bool interleave)
+                                                           uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
 {
     __shared__ uint32_t qmem[kWaves * kQWords * kQ];
     /* LDS: the next round's blocks arrive by LDS-DMA into a per-wave 4 KiB
@@ -163,12 +162,12 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
     /* a wave owns `chunk` consecutive tiles; the grid covers every tile once
      * and the hardware dispatcher balances the waves (no persistent grid to
      * size from an occupancy estimate) */
-    const Tiles tiles = wave_tiles(ntiles, chunk, kWaves, wave, interleave);
+    const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
     uint64_t tile = 0; /* local tile index */
     const uint64_t tlast = tiles.n;
     if (tile >= tlast) return;
     Queue q{qmem + wave * kQWords * kQ, 0u, 0u};
-    Walker wk;
+    Walker<IL> wk;
     wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + (LDS ? wave * kImage : 0u);
     auto load_blk = [&](const TileKeys &t, uint32_t b, u32x4 (&d)[4]) __attribute__((always_inline)) {
@@ -276,19 +275,19 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
  * (with long keys every lane of a tile usually needs it at once, so there is
  * no queue).
  */
+template <bool IL>
 __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
-                                                           uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk,
-                                                           bool interleave)
+                                                           uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
 {
     __shared__ __attribute__((aligned(16))) uint8_t kbuf[kWaves * kLineImage];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const Tiles tiles = wave_tiles(ntiles, chunk, kWaves, wave, interleave);
+    const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
     uint64_t tile = 0; /* local tile index */
     const uint64_t tlast = tiles.n;
     if (tile >= tlast) return;
-    Walker wk;
+    Walker<IL> wk;
     wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + wave * kLineImage;
     TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
@@ -374,12 +373,21 @@ hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, 
     const uint64_t grid = (ntiles + (uint64_t)kWaves * chunk - 1u) / ((uint64_t)kWaves * chunk);
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     (void)hipGetLastError();
-    if (var & 4)
-        hipLaunchKernelGGL(nc_md5_lines_kernel, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off, nkeys, d_out,
-                           ntiles, chunk, (var & 8) != 0);
-    else
-        hipLaunchKernelGGL(nc_md5_direct_kernel<false>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off,
-                           nkeys, d_out, ntiles, chunk, (var & 8) != 0);
+    const bool il = (var & 8) != 0;
+    if (var & 4) {
+        if (il)
+            hipLaunchKernelGGL(nc_md5_lines_kernel<true>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off,
+                               nkeys, d_out, ntiles, chunk);
+        else
+            hipLaunchKernelGGL(nc_md5_lines_kernel<false>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off,
+                               nkeys, d_out, ntiles, chunk);
+    } else if (il) {
+        hipLaunchKernelGGL((nc_md5_direct_kernel<false, true>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
+                           d_off, nkeys, d_out, ntiles, chunk);
+    } else {
+        hipLaunchKernelGGL((nc_md5_direct_kernel<false, false>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
+                           d_off, nkeys, d_out, ntiles, chunk);
+    }
     return hipGetLastError();
 }
 
