@@ -43,7 +43,7 @@ def gpu_hash(mode, keys_d, off_d):
                         (0, 0, 10624), (0, 0, 16512), (7, 0, 16512 | 2048 | 768), (0, 0, 16512 | 1792),
                         (0, 0, 65536 | (1 << 18)), (0, 1, 32 | (1 << 18)), (0, 0, 1 << 19),
                         (0, 0, (1 << 19) | (4 << 20)), (0, 0, (1 << 19) | (10 << 20)),
-                        (0, 0, (1 << 19) | (14 << 20))],
+                        (0, 0, (1 << 19) | (14 << 20)), (0, 0, 1 << 24), (0, 0, (1 << 24) | (9 << 20))],
                 ids=["persistent+sort", "auto", "workgroup", "grid37+sort+shiftadd", "shiftadd", "grid5+sort",
                      "sorted_bit", "regstage", "regstage+sort", "grid11+regstage+sort+shiftadd", "grid9+regstage",
                      "cached", "cached+sort", "regstage+cached", "grid7+regstage+cached+sort", "wavering",
@@ -51,7 +51,7 @@ def gpu_hash(mode, keys_d, off_d):
                      "wavering+cached", "wavering_w4_pair", "grid3+wavering_3_1_2_w4_pair", "wavering_w4",
                      "wavering_t64_w4", "wavering_t256_sorted", "grid7+wavering_t256_sorted_w4_6_2_3",
                      "wavering_t256_sorted_5_1_2", "workgroup_over3", "regstage+sort+over3", "direct",
-                     "direct_lines", "direct_il32", "direct_lines_il32"])
+                     "direct_lines", "direct_il32", "direct_lines_il32", "wsort", "wsort_il4"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)
@@ -237,7 +237,7 @@ def test_sort_and_grid_variants_agree_full_size(gpu):
                             (0, 1, 65536), (3, 1, 1), (0, 0, 1 << 17), (7, 0, 2176), (0, 0, 32), (0, 1, 32), (5, 1, 33), (13, 1, 32), (1024, 0, 32),
                             (1536, 0, 32), (2048, 1, 32), (0, 0, 64), (0, 1, 64), (0, 0, 96), (1536, 1, 96),
                             (0, 0, 128), (1, 0, 128), (7, 0, 384), (0, 0, 640), (2048, 0, 896), (0, 0, 129),
-                            (0, 0, 192)):
+                            (0, 0, 192), (0, 0, 1 << 24), (0, 0, (1 << 24) | (2 << 20)), (0, 0, (1 << 24) | (8 << 20))):
         L.lib().nc_gpuhash_set_tuning(grid, sort, var)
         out = t.hash_batch_device("fnv1a_64", kd, od)
         torch.cuda.synchronize()
@@ -264,7 +264,7 @@ def test_key_buffers_beyond_4gib(gpu):
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     try:
         for var in (0, 65536, 32, 128, 896, 2176, 1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (14 << 20),
-                    (1 << 19) | (8 << 20)):
+                    (1 << 19) | (8 << 20), 1 << 24):
             L.lib().nc_gpuhash_set_tuning(0, 0, var)
             for name in ("md5", "crc32", "fnv1a_64"):
                 t.hash_batch_device(name, kd, od, out, shape=spec.shape(256 * n))
@@ -362,6 +362,32 @@ def test_direct_ragged_tiles(gpu, oracle, var):
                         (70001, t.SynthSpec.fixed(47, 256))):
             keys, off = t.synth_host(spec, 3, n)
             kd, od = to_dev(keys, off, shift=3)
+            for m in MODES:
+                np.testing.assert_array_equal(gpu_hash(m, kd, od), oracle.batch(m, keys, off),
+                                              err_msg=f"var={var} n={n} spec={spec} mode={t.HASH_NAMES[m]}")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
+@pytest.mark.parametrize("var", [1 << 24, (1 << 24) | (1 << 20), (1 << 24) | (2 << 20), (1 << 24) | (3 << 20),
+                                 (1 << 24) | (8 << 20), (1 << 24) | (11 << 20)],
+                         ids=["wsort8", "wsort4", "wsort16", "wsort32", "wsort8_il", "wsort32_il"])
+def test_wsort_ragged_tiles(gpu, oracle, var):
+    """The wave-sorted pipeline (fnv x4 and one_at_a_time; the other modes take
+    their default pipeline) on batch sizes around its 256-key tile and the
+    per-wave tile count, with empty keys, Zipf and uniform lengths, tiles that
+    overflow the 6 KiB slab (the global fallback, alone and mixed with slab
+    tiles), a misaligned key buffer, against the oracle."""
+    L.lib().nc_gpuhash_set_tuning(0, 0, var)
+    try:
+        for n, spec in ((1, t.SynthSpec.uniform(50, 0, 3)), (63, t.SynthSpec.zipf(51)), (255, t.SynthSpec.zipf(52)),
+                        (256, t.SynthSpec.fixed(53, 24)), (257, t.SynthSpec.uniform(54, 0, 64)),
+                        (1023, t.SynthSpec.uniform(55, 0, 48)), (4097, t.SynthSpec.zipf(56)),
+                        (9000, t.SynthSpec.uniform(57, 0, 60)), (70001, t.SynthSpec.zipf(58)),
+                        (3000, t.SynthSpec.uniform(59, 0, 300)), (2049, t.SynthSpec.fixed(60, 25)),
+                        (600, t.SynthSpec.uniform(61, 0, 2000))):
+            keys, off = t.synth_host(spec, 3, n)
+            kd, od = to_dev(keys, off, shift=7)
             for m in MODES:
                 np.testing.assert_array_equal(gpu_hash(m, kd, od), oracle.batch(m, keys, off),
                                               err_msg=f"var={var} n={n} spec={spec} mode={t.HASH_NAMES[m]}")

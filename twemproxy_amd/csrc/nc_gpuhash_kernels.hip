@@ -1755,6 +1755,14 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
                   hipStream_t stream, int var);
 } // namespace nc_bytes
 
+namespace nc_wsort {
+/* fnv x4 and one_at_a_time on the wave-sorted pipeline (nc_wsort_kernels.hip):
+ * 256-key tiles per wave, length-sorted rounds */
+bool supports(int mode);
+hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
+                  hipStream_t stream, int var);
+} // namespace nc_wsort
+
 namespace {
 using nc_tu::g_grid_cap;
 using nc_tu::g_num_cus;
@@ -1776,6 +1784,7 @@ constexpr int kVarDirect = kVarMd5Direct;
 constexpr int kVarDirectLds = 4 << 20; /* its LDS-DMA block image (long keys) */
 constexpr int kVarDirectIl32 = (8 | 2) << 20; /* a wave's tiles interleaved over the grid, 32 per wave (nc_direct.h
                                                  wave_tiles) */
+constexpr int kVarWsort = 1 << 24; /* the wave-sorted pipeline (nc_wsort_kernels.hip); options in bits 20-23 */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2162,7 +2171,9 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
         if (mode == NC_GPUHASH_MD5) return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
         if (nc_bytes::supports(mode)) return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
     }
-    var &= ~(kVarDirect | (15 << 20));
+    if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))
+        return nc_wsort::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
+    var &= ~(kVarDirect | kVarWsort | (15 << 20));
     const bool sort = sort_enabled() || (var & kVarSorted) != 0;
     var &= ~(kVarWorkgroup | kVarSorted); /* kVarOver rides along to launch_kernel */
     /* the wave ring DMAs offsets 16 bytes per lane: it needs 16-byte aligned
