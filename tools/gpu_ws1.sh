@@ -1,7 +1,5 @@
 set -u
-O=gpurun_out/ws7
+O=gpurun_out/rs1
 mkdir -p $O
-timeout -k 10 120 python3 tools/ws_debug.py 1048576 16777216 > $O/debug.log 2>&1 || exit $?
-timeout -k 10 300 python3 tools/ab.py --configs C2 --modes fnv1a_64 --variants 0,16777216,17825792,18874368,20971520,21037056 > $O/c2.jsonl 2>&1 || exit $?
-timeout -k 10 300 python3 tools/ab.py --configs C2 --modes one_at_a_time,fnv1_32 --variants 0,16777216,17825792 >> $O/c2.jsonl 2>&1 || exit $?
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "wsort or sort_and_grid or corpus" > $O/pytest.log 2>&1
+timeout -k 10 400 python3 tools/ab.py --configs C2 --modes fnv1a_64 --variants 0,33554560,33554816,33555584,33555840,33555072,32896 > $O/c2.jsonl 2>&1 || exit $?
+timeout -k 10 300 python3 tools/ab.py --configs C2 --modes one_at_a_time,fnv1_32 --variants 0,33554560,33554816,16777216 >> $O/c2.jsonl 2>&1 || exit $?

@@ -2152,7 +2152,11 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
     /* varying lengths: a wave runs as long as its longest key; length-grouped
      * tiles and oversubscribed grids rebalance that */
     if (mean < 22u) { /* C2 */
-        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarWorkgroup | kVarSorted | kVarOver;
+        /* one_at_a_time (the most VALU per byte): the wave-sorted pipeline,
+         * whose 6 KiB slab holds a 256-key tile of keys up to ~20 B on average
+         * (C2 0.585 -> 0.505 ms; fnv1a_64 stays 4 % faster on the workgroup
+         * x3, profiles/r02_wsort.jsonl) */
+        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return mean < 20u ? kVarWsort : kVarWorkgroup | kVarSorted | kVarOver;
         return kVarWorkgroup | kVarOver;
     }
     if (crc || mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarRegStaged | kVarOver;
