@@ -61,6 +61,10 @@ rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const u
  * tiles in two sorted rounds); bit 16: the plain workgroup
  * pipeline as an explicit choice; bit 17: length-grouped tiles, as sort = 1;
  * bit 18: workgroup pipelines launch three resident sets of workgroups;
+ * bit 19: the direct per-lane pipeline (md5 and the byte-serial modes), bits
+ * 20-23 its options (tiles per wave, 128-byte line image, grid interleave);
+ * bit 24: the wave-sorted pipeline (fnv x4, one_at_a_time), bits 20-21 its
+ * tiles per wave, bit 22 DIAGNOSTIC no-hash build (fnv1a_64);
  * -1 = keep). */
 rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
