@@ -153,7 +153,7 @@ __device__ __forceinline__ void sort_tile(uint32_t *es, uint8_t *ps, uint32_t *c
 
 } // namespace
 
-template <int MODE, bool NOHASH>
+template <int MODE, bool NOHASH, bool IL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void nc_wsort_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ off, uint64_t nkeys, uint32_t *__restrict__ out,
     uint64_t ntiles, uint32_t chunk)
@@ -162,13 +162,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     WaveLds &L = lds_all[wave];
-    /* wave w takes `chunk` consecutive tiles (a grid of many short-lived
-     * waves: a new wave's first loads overlap the others' hashing) */
-    const uint64_t w = (uint64_t)blockIdx.x * kWaves + wave;
-    const uint64_t tb = w * chunk;
-    if (tb >= ntiles) return;
-    const uint64_t n = ntiles - tb < chunk ? ntiles - tb : chunk;
-    auto k0_of = [&](uint64_t j) __attribute__((always_inline)) { return (tb + (j < n ? j : n - 1u)) * kTK; };
+    /* wave w takes `chunk` tiles: consecutive ones (a grid of many
+     * short-lived waves: a new wave's first loads overlap the others'
+     * hashing), or (IL) tiles w, w + W, w + 2W, ... of the grid's W waves, so
+     * the resident waves stream neighbouring tiles (nc_direct.h wave_tiles) */
+    const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
+    const uint64_t n = tiles.n;
+    if (n == 0) return;
+    auto k0_of = [&](uint64_t j) __attribute__((always_inline)) { return tiles.at(j < n ? j : n - 1u) * kTK; };
 
     /* slab loads of a tile: the 16-byte chunks from abase up to its end
      * (rounded up: a load that crosses the resource's end reads zeros WHOLE;
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
 
 namespace nc_wsort {
 
-template <int MODE, bool NH>
+template <int MODE, bool NH, bool IL>
 hipError_t launch_k(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
                     uint32_t chunk)
 {
@@ -279,7 +280,7 @@ hipError_t launch_k(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys
     if (grid == 0) return hipSuccess;
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     (void)hipGetLastError();
-    hipLaunchKernelGGL((nc_wsort_kernel<MODE, NH>), dim3((unsigned)grid), dim3(64 * kWaves), 0, stream, d_keys, d_off,
+    hipLaunchKernelGGL((nc_wsort_kernel<MODE, NH, IL>), dim3((unsigned)grid), dim3(64 * kWaves), 0, stream, d_keys, d_off,
                        nkeys, d_out, ntiles, chunk);
     return hipGetLastError();
 }
@@ -290,15 +291,19 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
 {
     static const uint32_t kChunk[4] = {4, 2, 8, 16};
     const uint32_t chunk = kChunk[var & 3];
+    const bool il = (var & 8) != 0;
     if (var & 4) { /* DIAGNOSTIC: no hashing (outputs are key lengths), fnv1a_64 only */
         if (MODE != NC_GPUHASH_FNV1A_64) return hipErrorInvalidValue;
-        return launch_k<NC_GPUHASH_FNV1A_64, true>(d_keys, d_off, nkeys, d_out, stream, chunk);
+        return il ? launch_k<NC_GPUHASH_FNV1A_64, true, true>(d_keys, d_off, nkeys, d_out, stream, chunk)
+                  : launch_k<NC_GPUHASH_FNV1A_64, true, false>(d_keys, d_off, nkeys, d_out, stream, chunk);
     }
-    return launch_k<MODE, false>(d_keys, d_off, nkeys, d_out, stream, chunk);
+    return il ? launch_k<MODE, false, true>(d_keys, d_off, nkeys, d_out, stream, chunk)
+              : launch_k<MODE, false, false>(d_keys, d_off, nkeys, d_out, stream, chunk);
 }
 
 /* var: bits 0-1 tiles per wave (4, 2, 8, 16), bit 2 DIAGNOSTIC no-hash
- * build (fnv1a_64). nkeys < 2^32. */
+ * build (fnv1a_64), bit 3 a wave's tiles interleaved over the grid.
+ * nkeys < 2^32. */
 bool supports(int mode)
 {
     switch (mode) {
