@@ -64,8 +64,9 @@ rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const u
  * bit 19: the direct per-lane pipeline (md5 and the byte-serial modes), bits
  * 20-23 its options (tiles per wave, 128-byte line image, grid interleave);
  * bit 24: the wave-sorted pipeline (fnv x4, one_at_a_time), bits 20-21 its
- * tiles per wave, bit 22 DIAGNOSTIC no-hash build (fnv1a_64);
- * -1 = keep). */
+ * tiles per wave, bit 22 DIAGNOSTIC no-hash build (fnv1a_64), bit 23 its
+ * tiles interleaved over the grid; bit 26: md5 without its fixed-length
+ * specialisation (A/B); -1 = keep). */
 rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
 #ifdef __cplusplus

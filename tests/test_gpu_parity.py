@@ -393,3 +393,38 @@ def test_wsort_ragged_tiles(gpu, oracle, var):
                                               err_msg=f"var={var} n={n} spec={spec} mode={t.HASH_NAMES[m]}")
     finally:
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
+@pytest.mark.parametrize("fl", [16, 20, 24, 32, 40, 48])
+def test_md5_fixed_length_specialisation(gpu, oracle, fl):
+    """md5's fixed-length instantiations (picked by a shape whose min == max)
+    on batches around the 64-key tile, misaligned, and with the shape
+    claiming fixed lengths while some tiles hold other lengths (each tile
+    checks its keys and takes the generic path), against the oracle; the
+    generic path (variant bit 26) on the same keys."""
+    rng = np.random.default_rng(fl)
+    for n in (1, 63, 64, 65, 1000, 4097):
+        keys, off = t.synth_host(t.SynthSpec.fixed(70 + fl, fl), 3, n)
+        lens = np.full(n, fl)
+        if n >= 64:  # a few odd lengths in a few tiles
+            for i in rng.choice(n, size=3, replace=False):
+                lens[i] = int(rng.integers(0, 120))
+            blob = keys[: off[-1]].tobytes()
+            parts, pos = [], 0
+            for ln in lens:
+                parts.append((blob * 3)[pos: pos + int(ln)])
+                pos += fl
+            keys, off = t.pack_keys(parts)
+        kd, od = to_dev(keys, off, shift=5)
+        want = oracle.batch(1, keys, off)
+        for var in (0, (1 << 19) | (1 << 26)):
+            L.lib().nc_gpuhash_set_tuning(0, 0, var)
+            try:
+                got = t.hash_batch_device("md5", kd, od, shape=(int(off[-1]), fl, fl))
+                import torch
+
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want,
+                                              err_msg=f"fl={fl} n={n} var={var}")
+            finally:
+                L.lib().nc_gpuhash_set_tuning(0, 0, 0)

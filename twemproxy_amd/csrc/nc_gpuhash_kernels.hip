@@ -1745,7 +1745,7 @@ namespace nc_md5 {
 /* md5 on the direct per-lane block pipeline (nc_md5_kernels.hip); keys is any
  * byte address, nkeys < 2^32 */
 hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
-                  int var);
+                  int var, uint32_t fl);
 } // namespace nc_md5
 
 namespace nc_bytes {
@@ -1785,6 +1785,7 @@ constexpr int kVarDirectLds = 4 << 20; /* its LDS-DMA block image (long keys) */
 constexpr int kVarDirectIl32 = (8 | 2) << 20; /* a wave's tiles interleaved over the grid, 32 per wave (nc_direct.h
                                                  wave_tiles) */
 constexpr int kVarWsort = 1 << 24; /* the wave-sorted pipeline (nc_wsort_kernels.hip); options in bits 20-23 */
+constexpr int kVarNoFixedLen = 1 << 26; /* md5: no fixed-length specialisation (A/B) */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2172,12 +2173,19 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
     const int tuned = load_i(&g_variant);
     int var = tuned != 0 ? tuned : pick_variant(mode, nkeys, shape);
     if ((var & kVarDirect) != 0 && nkeys < (1ull << 32)) { /* bits 20-23: options */
-        if (mode == NC_GPUHASH_MD5) return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
+        if (mode == NC_GPUHASH_MD5) {
+            /* fixed-length keys (the caller's shape; bit 26 turns it off for A/B) */
+            const uint32_t fl = shape != nullptr && nkeys != 0 && shape->min_len == shape->max_len &&
+                                        (var & kVarNoFixedLen) == 0
+                                    ? (uint32_t)shape->min_len
+                                    : 0u;
+            return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15, fl);
+        }
         if (nc_bytes::supports(mode)) return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
     }
     if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))
         return nc_wsort::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
-    var &= ~(kVarDirect | kVarWsort | (15 << 20));
+    var &= ~(kVarDirect | kVarWsort | kVarNoFixedLen | (15 << 20));
     const bool sort = sort_enabled() || (var & kVarSorted) != 0;
     var &= ~(kVarWorkgroup | kVarSorted); /* kVarOver rides along to launch_kernel */
     /* the wave ring DMAs offsets 16 bytes per lane: it needs 16-byte aligned

@@ -133,6 +133,8 @@ __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__re
         w[0] = (len & 63u) == 0u ? 0x80u : 0u;
         w[14] = len << 3;
         w[15] = len >> 29;
+        /* (the generic block: md5_tail_final_a costs this kernel three VGPRs,
+         * one wave per SIMD) */
         __builtin_nontemporal_store(md5_block_final_a(st, w), out + idx);
     }
     q.head = (q.head + n) & (kQ - 1u);
@@ -148,7 +150,7 @@ __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__re
  * key i = keys[off[i], off[i+1]); keys stays readable NC_GPUHASH_PAD bytes
  * past off[nkeys]. A tile of 64 keys spans less than 4 GiB.
  */
-template <bool LDS, bool IL>
+template <bool LDS, bool IL, int FL = 0>
 __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
                                                            uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
@@ -199,7 +201,21 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
         uint32_t w[16];
         if constexpr (LDS) wk.read_img(img, d); /* this round's block, DMA'd during the previous round */
         const u32x4 (&cur)[4] = d;
-        if (act) {
+        /* FL: a tile whose keys all have FL bytes (checked: the shape only
+         * picks the instantiation) takes its data words as loaded, the
+         * boundary word by one constant perm, and constants for the rest */
+        bool fl_tile = false;
+        if constexpr (FL > 0) fl_tile = __ballot(cur_t.valid && cur_t.len != (uint32_t)FL) == 0ull;
+        if (fl_tile) {
+            if constexpr (FL > 0) {
+#pragma unroll
+                for (int t = 0; t < FL / 4; t++) w[t] = cur[t >> 2][t & 3];
+                if constexpr (FL % 4 != 0) {
+                    constexpr uint32_t bnd = FL % 4 == 1 ? kBoundary1 : (FL % 4 == 2 ? kBoundary2 : kBoundary3);
+                    w[FL / 4] = __builtin_amdgcn_perm(cur[(FL / 4) >> 2][(FL / 4) & 3], pad_src, bnd);
+                }
+            }
+        } else if (act) {
             msg_words(cur, rem < 64 ? rem : 64, pad_src, w);
             const bool fin = rem <= 55; /* the bit length fits behind the pad */
             if (fin) {
@@ -215,7 +231,16 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
          * tile still has blocks it re-reads the next tile's words, which
          * keeps the per-round load count fixed */
         no = wk.load_off(more ? tile + 1u : tile + 2u);
-        if (act) {
+        if (fl_tile) {
+            if constexpr (FL > 0) {
+                if (act) {
+                    uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+                    md5_steps_fl<FL>(v, w, std::make_integer_sequence<int, 61>{});
+                    const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
+                    __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
+                }
+            }
+        } else if (act) {
             const bool fin = rem <= 55;
             /* steps 0..60 for every lane; a key that ends here is done (A's
              * last update is step 60), the others run steps 61..63 */
@@ -342,7 +367,7 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
             w[14] = cur_t.len << 3;
             w[15] = cur_t.len >> 29;
             const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
-            __builtin_amdgcn_raw_buffer_store_b32(md5_block_final_a(st, w), rout, (int)(lane * 4u), 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(md5_tail_final_a(st, w), rout, (int)(lane * 4u), 0, kAuxNt);
         }
         if (more) {
             b++;
@@ -362,10 +387,21 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
 
 namespace nc_md5 {
 
+template <int FL>
+void launch_fl(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
+               uint64_t grid, uint64_t ntiles, uint32_t chunk)
+{
+    hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, FL>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
+                       d_off, nkeys, d_out, ntiles, chunk);
+}
+
 /* var: bits 0-1 tiles per wave (0: 16, 1: 8, 2: 32, 3: 64); bit 2: the LDS-DMA
- * variant (long keys) */
+ * variant (long keys); bit 3 tiles interleaved over the grid. fl: the batch's
+ * fixed key length if the caller's shape says so (0: unknown or varying);
+ * 16, 20, 24, 32, 40 and 48 have specialised instantiations (each tile still
+ * checks its lengths) */
 hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
-                  int var)
+                  int var, uint32_t fl)
 {
     static const uint32_t kChunk[4] = {16, 8, 32, 64};
     const uint32_t chunk = kChunk[var & 3];
@@ -384,6 +420,15 @@ hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, 
     } else if (il) {
         hipLaunchKernelGGL((nc_md5_direct_kernel<false, true>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
                            d_off, nkeys, d_out, ntiles, chunk);
+    } else if (fl == 16 || fl == 20 || fl == 24 || fl == 32 || fl == 40 || fl == 48) {
+        switch (fl) {
+        case 16: launch_fl<16>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        case 20: launch_fl<20>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        case 24: launch_fl<24>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        case 32: launch_fl<32>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        case 40: launch_fl<40>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        default: launch_fl<48>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        }
     } else {
         hipLaunchKernelGGL((nc_md5_direct_kernel<false, false>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
                            d_off, nkeys, d_out, ntiles, chunk);

@@ -58,6 +58,87 @@ __device__ __forceinline__ void md5_steps_from61(uint32_t (&v)[4], const uint32_
     (md5_step<61 + I>(v, w), ...);
 }
 
+/* ---- fixed-length keys of FL bytes (1..55): one block, and every message
+ * word past the key's data is a compile-time constant: zeros, the 0x80 pad
+ * when it starts a word, the bit length FL * 8 in word 14
+ * (src/hashkit/nc_md5.c:249-274). Such a word's w + T folds into one
+ * constant (an SGPR operand of the v_add3): four VALU per step instead of
+ * five. */
+template <int FL>
+constexpr bool fl_const(int k)
+{
+    return k > FL / 4 || (k == FL / 4 && FL % 4 == 0);
+}
+
+template <int FL>
+constexpr uint32_t fl_word(int k)
+{
+    return k == 14 ? (uint32_t)FL * 8u : ((k == FL / 4 && FL % 4 == 0) ? 0x80u : 0u);
+}
+
+template <int I, int FL>
+__device__ __forceinline__ void md5_step_fl(uint32_t (&v)[4], const uint32_t (&w)[16])
+{
+    static_assert(FL >= 1 && FL <= 55, "one block with the length behind the pad");
+    constexpr int k = kM[I];
+    if constexpr (fl_const<FL>(k)) {
+        constexpr int u = (4 - (I & 3)) & 3;
+        const uint32_t b = v[(u + 1) & 3], c = v[(u + 2) & 3], d = v[(u + 3) & 3];
+        uint32_t f;
+        if constexpr (I < 16) f = NC_MD5_F(b, c, d);
+        else if constexpr (I < 32) f = NC_MD5_G(b, c, d);
+        else if constexpr (I < 48) f = NC_MD5_H(b, c, d);
+        else f = NC_MD5_I(b, c, d);
+        constexpr uint32_t wt = fl_word<FL>(k) + kT[I];
+        v[u] = nc_rotl(v[u] + f + wt, kS[I]) + b;
+    } else {
+        md5_step<I>(v, w);
+    }
+}
+
+template <int FL, int... I>
+__device__ __forceinline__ void md5_steps_fl(uint32_t (&v)[4], const uint32_t (&w)[16],
+                                             std::integer_sequence<int, I...>)
+{
+    (md5_step_fl<I, FL>(v, w), ...);
+}
+
+/* ---- the data-free last block of a key (src/hashkit/nc_md5.c:263-274):
+ * words 1..13 are zero, so their steps take w + T as one constant; words 0
+ * (0x80 or 0), 14 and 15 (the bit length) stay per lane ---- */
+template <int I>
+__device__ __forceinline__ void md5_step_tail(uint32_t (&v)[4], const uint32_t (&w)[16])
+{
+    constexpr int k = kM[I];
+    if constexpr (k >= 1 && k <= 13) {
+        constexpr int u = (4 - (I & 3)) & 3;
+        const uint32_t b = v[(u + 1) & 3], c = v[(u + 2) & 3], d = v[(u + 3) & 3];
+        uint32_t f;
+        if constexpr (I < 16) f = NC_MD5_F(b, c, d);
+        else if constexpr (I < 32) f = NC_MD5_G(b, c, d);
+        else if constexpr (I < 48) f = NC_MD5_H(b, c, d);
+        else f = NC_MD5_I(b, c, d);
+        v[u] = nc_rotl(v[u] + f + kT[I], kS[I]) + b;
+    } else {
+        md5_step<I>(v, w);
+    }
+}
+
+template <int... I>
+__device__ __forceinline__ void md5_steps_tail(uint32_t (&v)[4], const uint32_t (&w)[16],
+                                               std::integer_sequence<int, I...>)
+{
+    (md5_step_tail<I>(v, w), ...);
+}
+
+/* A after a data-free last block w (words 1..13 zero) */
+__device__ __forceinline__ uint32_t md5_tail_final_a(const uint32_t (&st)[4], const uint32_t (&w)[16])
+{
+    uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+    md5_steps_tail(v, w, std::make_integer_sequence<int, 61>{});
+    return st[0] + v[0];
+}
+
 /* final block: only A is returned, and A's last update is step 60 */
 __device__ __forceinline__ uint32_t md5_block_final_a(const uint32_t (&st)[4], const uint32_t (&w)[16])
 {
