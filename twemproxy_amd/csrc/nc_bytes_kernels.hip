@@ -119,12 +119,11 @@ __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], 
  * other register set, or the LDS image) while this one computes.
  */
 /* CO (registers only): a tile of short keys whose bytes all lie in the first
- * kCoSpan bytes from its first key, each key starting dword aligned within
- * that span (fixed 4k-byte keys up to 32 B: C3), is staged by two COALESCED 16-byte
+ * kCoSpan bytes from its first key, each key starting 16-byte aligned within
+ * that span (fixed 16/32-byte keys: C3), is staged by two COALESCED 16-byte
  * loads per lane (1 KiB per wave instruction) instead of per-lane loads at
  * the key stride, then handed to its lanes through a wave-private 2 KiB LDS
- * slab (ds_write_b128; ds_read_b128 at the key's offset when every key is
- * 16-byte aligned, else ds_read_b32). The check is a
+ * slab (ds_write_b128, ds_read_b128 at the key's offset). The check is a
  * ballot per tile; any other tile takes the per-lane loads. */
 constexpr uint32_t kCoSpan = 2048u;
 
@@ -156,13 +155,11 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
     uint8_t *const img = kbuf + (LDS ? wave * kLineImage : 0u);
     u32x4 *const slab = cbuf + (CO ? wave * (kCoSpan / 16u) : 0u);
 
-    /* CO: every lane's key of tile t fits the coalesced span, dword aligned
-     * (the partial last tile and multi-round keys never qualify): 0 no, 1 every
-     * key dword aligned, 2 every key 16-byte aligned */
+    /* CO: every lane's key of tile t fits the coalesced span, 16-byte aligned
+     * (the partial last tile and multi-round keys never qualify) */
     auto co_tile = [&](const TileKeys &t) __attribute__((always_inline)) {
-        const bool ok = t.valid && (t.srel & 3u) == 0u && t.len <= 64u && t.srel + t.len <= kCoSpan;
-        if (__ballot(!ok) != 0ull) return 0u;
-        return __ballot((t.srel & 15u) != 0u) == 0ull ? 2u : 1u;
+        const bool ok = t.valid && (t.srel & 15u) == 0u && t.len <= 64u && t.srel + t.len <= kCoSpan;
+        return __ballot(!ok) == 0ull;
     };
     /* the tile's first kCoSpan bytes, lane-interleaved: chunk lane + 64j */
     auto co_load = [&](const TileKeys &t, u32x4 (&d)[4]) __attribute__((always_inline)) {
@@ -171,28 +168,21 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
         d[1] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(1024u + lane * 16u), 0, kAuxNt);
     };
     /* through the wave's slab to the lane that owns each key */
-    auto co_scatter = [&](const TileKeys &t, uint32_t co, u32x4 (&d)[4]) __attribute__((always_inline)) {
+    auto co_scatter = [&](const TileKeys &t, u32x4 (&d)[4]) __attribute__((always_inline)) {
         __builtin_amdgcn_wave_barrier(); /* the previous tile's reads before these writes */
         slab[lane] = d[0];
         slab[64u + lane] = d[1];
         __builtin_amdgcn_wave_barrier(); /* every lane's writes before the reads (LDS runs a wave's ops in order) */
-        if (co == 2u) {
-            const u32x4 *k = slab + (t.srel >> 4);
+        const u32x4 *k = slab + (t.srel >> 4);
 #pragma unroll
-            for (uint32_t c = 0; c < 4u; c++)
-                if (t.len > 16u * c) d[c] = k[c];
-        } else { /* dword reads (a chunk's tail may read past the key: masked later) */
-            const uint32_t *k = reinterpret_cast<const uint32_t *>(slab) + (t.srel >> 2);
-#pragma unroll
-            for (uint32_t c = 0; c < 4u; c++)
-                if (t.len > 16u * c) d[c] = u32x4{k[4u * c], k[4u * c + 1u], k[4u * c + 2u], k[4u * c + 3u]};
-        }
+        for (uint32_t c = 0; c < 4u; c++)
+            if (t.len > 16u * c) d[c] = k[c];
     };
 
     TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
     Offs no = wk.load_off(tile + 1u);
     u32x4 da[4], db[4];
-    uint32_t cur_co = 0; /* CO: cur's registers hold the coalesced span (co_tile) */
+    bool cur_co = false; /* CO: cur's registers hold the coalesced span */
     if constexpr (LDS) {
         wk.dma_lines(cur_t, 0u, img);
     } else if constexpr (CO) {
@@ -210,13 +200,13 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
     auto round = [&](u32x4 (&cur)[4], u32x4 (&nxt)[4]) __attribute__((always_inline)) {
         const bool more = __ballot(cur_t.valid && cur_t.len > RB * (b + 1u)) != 0ull;
         const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
-        uint32_t nxt_co = 0;
+        bool nxt_co = false;
         if constexpr (LDS) {
             wk.read_lines(img, cur, nxt);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the image's reads are done */
             wk.dma_lines(more ? cur_t : nxt_t, more ? b + 1u : 0u, img);
         } else if constexpr (CO) {
-            nxt_co = more ? 0u : co_tile(nxt_t);
+            nxt_co = !more && co_tile(nxt_t);
             if (nxt_co) co_load(nxt_t, nxt);
             else wk.load_regs(more ? cur_t : nxt_t, more ? b + 1u : 0u, nxt);
         } else {
@@ -227,7 +217,7 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
         no = wk.load_off(more ? tile + 1u : tile + 2u);
 
         if constexpr (CO) {
-            if (cur_co) co_scatter(cur_t, cur_co, cur);
+            if (cur_co) co_scatter(cur_t, cur);
         }
         const int32_t rem = (int32_t)cur_t.len - (int32_t)RB * (int32_t)b;
         if (cur_t.valid && (rem > 0 || (b == 0u && cur_t.len == 0u))) {
