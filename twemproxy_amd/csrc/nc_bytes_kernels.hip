@@ -169,10 +169,8 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
     };
     /* through the wave's slab to the lane that owns each key */
     auto co_scatter = [&](const TileKeys &t, u32x4 (&d)[4]) __attribute__((always_inline)) {
-        __builtin_amdgcn_wave_barrier(); /* the previous tile's reads before these writes */
         slab[lane] = d[0];
         slab[64u + lane] = d[1];
-        __builtin_amdgcn_wave_barrier(); /* every lane's writes before the reads (LDS runs a wave's ops in order) */
         const u32x4 *k = slab + (t.srel >> 4);
 #pragma unroll
         for (uint32_t c = 0; c < 4u; c++)
