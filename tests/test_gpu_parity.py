@@ -43,8 +43,7 @@ def gpu_hash(mode, keys_d, off_d):
                         (0, 0, 10624), (0, 0, 16512), (7, 0, 16512 | 2048 | 768), (0, 0, 16512 | 1792),
                         (0, 0, 65536 | (1 << 18)), (0, 1, 32 | (1 << 18)), (0, 0, 1 << 19),
                         (0, 0, (1 << 19) | (4 << 20)), (0, 0, (1 << 19) | (10 << 20)),
-                        (0, 0, (1 << 19) | (14 << 20)), (0, 0, 1 << 24), (0, 0, (1 << 24) | (9 << 20)),
-                        (0, 0, (1 << 19) | (10 << 20) | (1 << 25))],
+                        (0, 0, (1 << 19) | (14 << 20)), (0, 0, 1 << 24), (0, 0, (1 << 24) | (9 << 20))],
                 ids=["persistent+sort", "auto", "workgroup", "grid37+sort+shiftadd", "shiftadd", "grid5+sort",
                      "sorted_bit", "regstage", "regstage+sort", "grid11+regstage+sort+shiftadd", "grid9+regstage",
                      "cached", "cached+sort", "regstage+cached", "grid7+regstage+cached+sort", "wavering",
@@ -52,7 +51,7 @@ def gpu_hash(mode, keys_d, off_d):
                      "wavering+cached", "wavering_w4_pair", "grid3+wavering_3_1_2_w4_pair", "wavering_w4",
                      "wavering_t64_w4", "wavering_t256_sorted", "grid7+wavering_t256_sorted_w4_6_2_3",
                      "wavering_t256_sorted_5_1_2", "workgroup_over3", "regstage+sort+over3", "direct",
-                     "direct_lines", "direct_il32", "direct_lines_il32", "wsort", "wsort_il4", "direct_co_il32"])
+                     "direct_lines", "direct_il32", "direct_lines_il32", "wsort", "wsort_il4"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)
@@ -347,24 +346,20 @@ def test_wave_ring_ragged_tiles(gpu, oracle, var):
 
 
 @pytest.mark.parametrize("var", [1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (8 << 20), (1 << 19) | (10 << 20),
-                                 (1 << 19) | (11 << 20), (1 << 19) | (14 << 20), (1 << 19) | (9 << 20),
-                                 (1 << 19) | (1 << 25), (1 << 19) | (10 << 20) | (1 << 25)],
-                         ids=["direct", "lines", "il16", "il32", "il64", "lines_il32", "il8", "co", "co_il32"])
+                                 (1 << 19) | (11 << 20), (1 << 19) | (14 << 20), (1 << 19) | (9 << 20)],
+                         ids=["direct", "lines", "il16", "il32", "il64", "lines_il32", "il8"])
 def test_direct_ragged_tiles(gpu, oracle, var):
     """The direct per-lane pipelines (md5 and the byte-serial modes; the other
     modes take their default pipeline), consecutive or grid-interleaved tiles
-    per wave, with or without the coalesced staging of short tiles (fixed 16 /
-    32-byte keys take it, partial tiles and other lengths fall back per tile),
-    on batch sizes around the 64-key tile and the per-workgroup tile count,
-    with empty keys, one-block, multi-block and padding-only-block keys, a
-    misaligned key buffer, against the oracle."""
+    per wave, on batch sizes around the 64-key tile and the per-workgroup tile
+    count, with empty keys, one-block, multi-block and padding-only-block keys,
+    a misaligned key buffer, against the oracle."""
     L.lib().nc_gpuhash_set_tuning(0, 0, var)
     try:
         for n, spec in ((1, t.SynthSpec.uniform(40, 0, 3)), (63, t.SynthSpec.zipf(41)), (64, t.SynthSpec.fixed(42, 32)),
                         (65, t.SynthSpec.uniform(43, 0, 300)), (129, t.SynthSpec.uniform(44, 50, 70)),
                         (4097, t.SynthSpec.zipf(45)), (70001, t.SynthSpec.uniform(46, 0, 200)),
-                        (70001, t.SynthSpec.fixed(47, 256)), (4097, t.SynthSpec.fixed(48, 16)),
-                        (70001, t.SynthSpec.fixed(49, 32)), (3000, t.SynthSpec.uniform(50, 0, 16))):
+                        (70001, t.SynthSpec.fixed(47, 256))):
             keys, off = t.synth_host(spec, 3, n)
             kd, od = to_dev(keys, off, shift=3)
             for m in MODES:
