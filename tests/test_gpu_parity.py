@@ -359,7 +359,9 @@ def test_direct_ragged_tiles(gpu, oracle, var):
         for n, spec in ((1, t.SynthSpec.uniform(40, 0, 3)), (63, t.SynthSpec.zipf(41)), (64, t.SynthSpec.fixed(42, 32)),
                         (65, t.SynthSpec.uniform(43, 0, 300)), (129, t.SynthSpec.uniform(44, 50, 70)),
                         (4097, t.SynthSpec.zipf(45)), (70001, t.SynthSpec.uniform(46, 0, 200)),
-                        (70001, t.SynthSpec.fixed(47, 256))):
+                        (70001, t.SynthSpec.fixed(47, 256)), (4097, t.SynthSpec.fixed(48, 16)),
+                        (70001, t.SynthSpec.fixed(49, 32)), (3000, t.SynthSpec.uniform(50, 0, 16)),
+                        (5000, t.SynthSpec.fixed(51, 20)), (4096, t.SynthSpec.fixed(52, 28))):
             keys, off = t.synth_host(spec, 3, n)
             kd, od = to_dev(keys, off, shift=3)
             for m in MODES:
