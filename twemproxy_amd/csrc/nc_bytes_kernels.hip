@@ -118,18 +118,8 @@ __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], 
  * key that has one into its state; the next round's block is in flight (the
  * other register set, or the LDS image) while this one computes.
  */
-/* CO (registers only): a tile of short keys whose bytes all lie in the first
- * kCoSpan bytes from its first key, each key starting dword aligned within
- * that span (fixed 4k-byte keys up to 32 B: C3), is staged by two COALESCED 16-byte
- * loads per lane (1 KiB per wave instruction) instead of per-lane loads at
- * the key stride, then handed to its lanes through a wave-private 2 KiB LDS
- * slab (ds_write_b128; ds_read_b128 at the key's offset when every key is
- * 16-byte aligned, else ds_read_b32). The check is a
- * ballot per tile; any other tile takes the per-lane loads. */
-constexpr uint32_t kCoSpan = 2048u;
-
-template <int MODE, bool LDS, bool IL, bool CO>
-__device__ __forceinline__ void bytes_direct_body(const uint8_t *__restrict__ keys,
+template <int MODE, bool LDS, bool IL>
+__global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__restrict__ keys,
                                                               const uint64_t *__restrict__ off, uint64_t nkeys,
                                                               uint32_t *__restrict__ out, uint64_t ntiles,
                                                               uint32_t chunk)
@@ -139,7 +129,6 @@ __device__ __forceinline__ void bytes_direct_body(const uint8_t *__restrict__ ke
     constexpr uint32_t RB = LDS ? 128u : 64u;
     __shared__ uint32_t tab[has_table<MODE>() ? kTabWords : 1];
     __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kLineImage : 16];
-    __shared__ u32x4 cbuf[CO ? kWaves * (kCoSpan / 16u) : 1];
     if constexpr (has_table<MODE>()) {
         nc_slice::fill<MODE, kCopies>(tab, threadIdx.x, 1024u);
         __syncthreads();
@@ -154,64 +143,12 @@ __device__ __forceinline__ void bytes_direct_body(const uint8_t *__restrict__ ke
     Walker<IL> wk;
     wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + (LDS ? wave * kLineImage : 0u);
-    u32x4 *const slab = cbuf + (CO ? wave * (kCoSpan / 16u) : 0u);
-
-    /* CO: every lane's key of tile t fits the coalesced span, dword aligned
-     * (the partial last tile and multi-round keys never qualify): 0 no, 1 every
-     * key dword aligned, 2 every key 16-byte aligned */
-    auto co_tile = [&](const TileKeys &t) __attribute__((always_inline)) {
-        const bool ok = t.valid && (t.srel & 3u) == 0u && t.len <= 64u && t.srel + t.len <= kCoSpan;
-        if (__ballot(!ok) != 0ull) return 0u;
-        return __ballot((t.srel & 15u) != 0u) == 0ull ? 2u : 1u;
-    };
-    /* one load sequence for both stagings, so every round issues the same
-     * vector-memory instructions (a wave-uniform branch between sequences of
-     * different lengths makes hipcc's waitcnt drain the next round's loads):
-     * CO, the tile's first kCoSpan bytes lane-interleaved (chunk lane + 64j,
-     * loads 0-1); else block b of the lane's key (loads 0-3, those holding key
-     * bytes) */
-    auto load_any = [&](uint32_t co, const TileKeys &t, uint32_t bb, u32x4 (&d)[4]) __attribute__((always_inline)) {
-        const rsrc_t r = make_rsrc(wk.keys + t.s0, wk.kbytes - t.s0);
-        const int32_t rem = (int32_t)t.len - 64 * (int32_t)bb;
-        const uint32_t vo = t.srel + 64u * bb;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const bool on = co ? k < 2 : rem > 16 * k;
-            const uint32_t o = co ? lane * 16u + 1024u * (uint32_t)k : vo + 16u * (uint32_t)k;
-            if (on) d[k] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)o, 0, 0);
-        }
-    };
-    /* through the wave's slab to the lane that owns each key */
-    auto co_scatter = [&](const TileKeys &t, uint32_t co, u32x4 (&d)[4]) __attribute__((always_inline)) {
-        __builtin_amdgcn_wave_barrier(); /* the previous tile's reads before these writes */
-        slab[lane] = d[0];
-        slab[64u + lane] = d[1];
-        __builtin_amdgcn_wave_barrier(); /* every lane's writes before the reads (LDS runs a wave's ops in order) */
-        if (co == 2u) {
-            const u32x4 *k = slab + (t.srel >> 4);
-#pragma unroll
-            for (uint32_t c = 0; c < 4u; c++)
-                if (t.len > 16u * c) d[c] = k[c];
-        } else { /* dword reads (a chunk's tail may read past the key: masked later) */
-            const uint32_t *k = reinterpret_cast<const uint32_t *>(slab) + (t.srel >> 2);
-#pragma unroll
-            for (uint32_t c = 0; c < 4u; c++)
-                if (t.len > 16u * c) d[c] = u32x4{k[4u * c], k[4u * c + 1u], k[4u * c + 2u], k[4u * c + 3u]};
-        }
-    };
 
     TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
     Offs no = wk.load_off(tile + 1u);
     u32x4 da[4], db[4];
-    uint32_t cur_co = 0; /* CO: cur's registers hold the coalesced span (co_tile) */
-    if constexpr (LDS) {
-        wk.dma_lines(cur_t, 0u, img);
-    } else if constexpr (CO) {
-        cur_co = co_tile(cur_t);
-        load_any(cur_co, cur_t, 0u, da);
-    } else {
-        wk.load_regs(cur_t, 0u, da);
-    }
+    if constexpr (LDS) wk.dma_lines(cur_t, 0u, img);
+    else wk.load_regs(cur_t, 0u, da);
     uint32_t b = 0;
     uint32_t h = init_state<MODE>();
 
@@ -220,14 +157,10 @@ __device__ __forceinline__ void bytes_direct_body(const uint8_t *__restrict__ ke
     auto round = [&](u32x4 (&cur)[4], u32x4 (&nxt)[4]) __attribute__((always_inline)) {
         const bool more = __ballot(cur_t.valid && cur_t.len > RB * (b + 1u)) != 0ull;
         const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
-        uint32_t nxt_co = 0;
         if constexpr (LDS) {
             wk.read_lines(img, cur, nxt);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the image's reads are done */
             wk.dma_lines(more ? cur_t : nxt_t, more ? b + 1u : 0u, img);
-        } else if constexpr (CO) {
-            nxt_co = more ? 0u : co_tile(nxt_t);
-            load_any(nxt_co, more ? cur_t : nxt_t, more ? b + 1u : 0u, nxt);
         } else {
             wk.load_regs(more ? cur_t : nxt_t, more ? b + 1u : 0u, nxt);
         }
@@ -235,9 +168,6 @@ __device__ __forceinline__ void bytes_direct_body(const uint8_t *__restrict__ ke
          * a re-read of the next tile's while this one still has blocks */
         no = wk.load_off(more ? tile + 1u : tile + 2u);
 
-        if constexpr (CO) {
-            if (cur_co) co_scatter(cur_t, cur_co, cur);
-        }
         const int32_t rem = (int32_t)cur_t.len - (int32_t)RB * (int32_t)b;
         if (cur_t.valid && (rem > 0 || (b == 0u && cur_t.len == 0u))) {
             h = block_step<MODE>(h, cur, rem, tab, lane4);
@@ -257,9 +187,6 @@ __device__ __forceinline__ void bytes_direct_body(const uint8_t *__restrict__ ke
             cur_t = nxt_t;
             h = init_state<MODE>();
         }
-        if constexpr (CO) {
-            cur_co = nxt_co;
-        }
     };
     for (;;) {
         if constexpr (LDS) {
@@ -272,25 +199,6 @@ __device__ __forceinline__ void bytes_direct_body(const uint8_t *__restrict__ ke
         if (tile >= tlast) break;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
-}
-
-template <int MODE, bool LDS, bool IL>
-__global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__restrict__ keys,
-                                                              const uint64_t *__restrict__ off, uint64_t nkeys,
-                                                              uint32_t *__restrict__ out, uint64_t ntiles,
-                                                              uint32_t chunk)
-{
-    bytes_direct_body<MODE, LDS, IL, false>(keys, off, nkeys, out, ntiles, chunk);
-}
-
-/* CO holds two staging forms in its registers: capped at 64 VGPRs so two
- * 1024-thread workgroups stay resident per CU */
-template <int MODE, bool IL>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void nc_bytes_direct_co_kernel(
-    const uint8_t *__restrict__ keys, const uint64_t *__restrict__ off, uint64_t nkeys, uint32_t *__restrict__ out,
-    uint64_t ntiles, uint32_t chunk)
-{
-    bytes_direct_body<MODE, false, IL, true>(keys, off, nkeys, out, ntiles, chunk);
 }
 
 namespace nc_bytes {
@@ -306,14 +214,7 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     (void)hipGetLastError();
     const bool il = (var & 8) != 0;
-    if ((var & 16) && !(var & 4)) { /* CO: coalesced staging of short tiles */
-        if (il)
-            hipLaunchKernelGGL((nc_bytes_direct_co_kernel<MODE, true>), dim3((unsigned)grid), dim3(1024), 0,
-                               stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
-        else
-            hipLaunchKernelGGL((nc_bytes_direct_co_kernel<MODE, false>), dim3((unsigned)grid), dim3(1024), 0,
-                               stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
-    } else if (var & 4) {
+    if (var & 4) {
         if (il)
             hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true>), dim3((unsigned)grid), dim3(1024), 0, stream,
                                d_keys, d_off, nkeys, d_out, ntiles, chunk);
@@ -332,8 +233,7 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
 
 /* the byte-serial modes on the direct pipeline; var: bits 0-1 tiles per wave
  * (16, 8, 32, 64), bit 2 the LDS-DMA block image (long keys), bit 3 a wave's
- * tiles interleaved over the grid (else consecutive), bit 4 coalesced staging
- * of short tiles (CO, registers only). nkeys < 2^32. */
+ * tiles interleaved over the grid (else consecutive). nkeys < 2^32. */
 bool supports(int mode)
 {
     switch (mode) {

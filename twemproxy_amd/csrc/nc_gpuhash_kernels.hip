@@ -1786,7 +1786,6 @@ constexpr int kVarDirectIl32 = (8 | 2) << 20; /* a wave's tiles interleaved over
                                                  wave_tiles) */
 constexpr int kVarWsort = 1 << 24; /* the wave-sorted pipeline (nc_wsort_kernels.hip); options in bits 20-23 */
 constexpr int kVarNoFixedLen = 1 << 26; /* md5: no fixed-length specialisation (A/B) */
-constexpr int kVarDirectCo = 1 << 25; /* byte-serial direct pipeline: coalesced staging of short tiles */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2182,13 +2181,11 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
                                     : 0u;
             return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15, fl);
         }
-        if (nc_bytes::supports(mode))
-            return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream,
-                                    ((var >> 20) & 15) | ((var & kVarDirectCo) != 0 ? 16 : 0));
+        if (nc_bytes::supports(mode)) return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
     }
     if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))
         return nc_wsort::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
-    var &= ~(kVarDirect | kVarWsort | kVarNoFixedLen | kVarDirectCo | (15 << 20));
+    var &= ~(kVarDirect | kVarWsort | kVarNoFixedLen | (15 << 20));
     const bool sort = sort_enabled() || (var & kVarSorted) != 0;
     var &= ~(kVarWorkgroup | kVarSorted); /* kVarOver rides along to launch_kernel */
     /* the wave ring DMAs offsets 16 bytes per lane: it needs 16-byte aligned
