@@ -5,7 +5,8 @@
 
 Configs: C1..C5, C4S = one GPU's C4 shard (2^25 x 256 B),
 F<len> fixed length (about 2 GiB), U<lo>-<hi> uniform lengths. Variant 0 is
-the shape policy; others are nc_gpuhash_set_tuning variant bits. For every
+the shape policy; others are nc_gpuhash_set_tuning variant bits, "v:g" the
+same with grid cap g (workgroup pipelines). For every
 (config, mode) the outputs of each variant are compared with the first
 variant's, key for key, and 512 sampled keys with the per-key host symbols.
 Prints one JSON line per (config, mode, variant): median / min kernel ms
@@ -54,7 +55,9 @@ def main():
         L.LIB_PATH = os.path.abspath(args.lib)
     import twemproxy_amd as t
 
-    variants = [int(v) for v in args.variants.split(",")]
+    # "v" or "v:g": variant bits v with grid cap g (nc_gpuhash_set_tuning)
+    variants = args.variants.split(",")
+    tune = {v: (int(v.split(":")[1]) if ":" in v else 0, int(v.split(":")[0])) for v in variants}
     rng = np.random.default_rng(1)
     for cfg in args.configs.split(","):
         spec, n = config(t, cfg, args.nkeys)
@@ -73,7 +76,7 @@ def main():
             res = {v: [] for v in variants}
             ok = {}
             for v in variants:
-                L.lib().nc_gpuhash_set_tuning(0, 0, v)
+                L.lib().nc_gpuhash_set_tuning(tune[v][0], 0, tune[v][1])
                 out.fill_(0)
                 t.hash_batch_device(mode, keys, off, out, shape=shape, key_end=kb)
                 torch.cuda.synchronize()
@@ -87,7 +90,7 @@ def main():
                     ok[v] = "same" if diff.size == 0 else f"DIFF {diff.size} first {int(diff[0])}"
             for _ in range(args.rounds):
                 for v in variants:
-                    L.lib().nc_gpuhash_set_tuning(0, 0, v)
+                    L.lib().nc_gpuhash_set_tuning(tune[v][0], 0, tune[v][1])
                     t.time_batch_device(mode, keys, off, out, 3, shape=shape)
                     res[v].append(t.time_batch_device(mode, keys, off, out, args.iters, shape=shape))
             for v in variants:
