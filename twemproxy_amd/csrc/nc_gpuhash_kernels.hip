@@ -1847,8 +1847,14 @@ hipError_t launch_kernel(const uint8_t *base, const uint64_t *off, uint64_t delt
     /* kVarOver: three resident sets of workgroups instead of one. The grid
      * stride still walks every tile, but workgroups whose keys ran short
      * finish early and new ones fill their slots: with varying key lengths
-     * (Zipf) this balances the CUs (C2 fnv1a_64: 0.49 -> 0.45 ms). */
-    const uint64_t over = (var & kVarOver) ? 3u : 1u;
+     * (Zipf) this balances the CUs (C2 fnv1a_64: 0.49 -> 0.45 ms). The
+     * plain hashing workgroup pipeline takes six sets (C2 fnv1a_64 0.450 ->
+     * 0.443 ms, hsieh 0.451 -> 0.443, crc32 0.649 -> 0.627 in a same-process
+     * grid sweep, profiles/r02_c2_grid_sweep.jsonl; four and eight sets are
+     * slower than three); the sorted, register-staged and dispatch forms keep
+     * three. */
+    constexpr uint64_t kOverSets = (!SORT && (VAR & 32) == 0 && wg_dist<VAR>() == kDistNone) ? 6u : 3u;
+    const uint64_t over = (var & kVarOver) ? kOverSets : 1u;
     uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu * over;
     if (grid > ntiles) grid = ntiles;
     (void)hipGetLastError(); /* a stale error from another library's call must not be reported as ours */
