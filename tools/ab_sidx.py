@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 PIPES = {"policy": 0, "ring": 1 << 28, "workgroup": 1 << 29}
+GRIDS = {}  # name -> grid cap (--grids: workgroup pipeline at these caps)
 
 
 def main():
@@ -24,7 +25,11 @@ def main():
     ap.add_argument("--tags", default="none")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--grids", default="", help="comma-separated grid caps for extra workgroup entries")
     args = ap.parse_args()
+    for g in filter(None, args.grids.split(",")):
+        PIPES[f"workgroup_g{g}"] = 1 << 29
+        GRIDS[f"workgroup_g{g}"] = int(g)
 
     import numpy as np
     import torch
@@ -52,7 +57,7 @@ def main():
                                             shape=shape, key_end=kb)
                     ref, res = None, {}
                     for name, v in PIPES.items():
-                        L.lib().nc_gpuhash_set_tuning(0, 0, v)
+                        L.lib().nc_gpuhash_set_tuning(GRIDS.get(name, 0), 0, v)
                         out.fill_(-1)
                         launch()
                         torch.cuda.synchronize()

@@ -1852,7 +1852,8 @@ hipError_t launch_kernel(const uint8_t *base, const uint64_t *off, uint64_t delt
      * 0.443 ms, hsieh 0.451 -> 0.443, crc32 0.649 -> 0.627 in a same-process
      * grid sweep, profiles/r02_c2_grid_sweep.jsonl; four and eight sets are
      * slower than three); the sorted, register-staged and dispatch forms keep
-     * three. */
+     * three (fused ketama server_idx on C2: 0.637 ms at three sets, 0.643 at
+     * six, profiles/r02f_sidx_grid_sweep.jsonl). */
     constexpr uint64_t kOverSets = (!SORT && (VAR & 32) == 0 && wg_dist<VAR>() == kDistNone) ? 6u : 3u;
     const uint64_t over = (var & kVarOver) ? kOverSets : 1u;
     uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu * over;
