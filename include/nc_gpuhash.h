@@ -219,10 +219,10 @@ void nc_gpuhash_redis_parser_destroy(nc_gpuhash_redis_parser_t *ps);
 
 /* Parse d_stream[0, nbytes); max_key_len is mbuf_data_size() (keys must be
  * shorter). Outputs as nc_gpuhash_mc_parse_device, with NC_GPUHASH_REDIS_*
- * statuses; d_req_status holds max_reqs entries. A stream of max_reqs ok
+ * statuses; d_req_status holds max_reqs + 1 entries. A stream of max_reqs ok
  * requests followed by a byte that starts no request is accepted: nreqs then
- * counts the failing request (max_reqs + 1) and first_error names it, but its
- * status has no slot and is not written. Blocks until done. */
+ * counts the failing request (max_reqs + 1), first_error names it and its
+ * status goes to d_req_status[max_reqs]. Blocks until done. */
 rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps, const uint8_t *d_stream, uint64_t nbytes,
                                         uint32_t max_key_len, uint8_t *d_keys, uint64_t *d_offsets,
                                         uint32_t *d_key_req, int32_t *d_req_status,

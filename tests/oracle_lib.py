@@ -198,3 +198,20 @@ class RefHashkit:
         out = np.empty(n, dtype=np.uint32)
         return float(self.lib.ref_time_batch(mode, keys.ctypes.data, offsets.ctypes.data, n, out.ctypes.data,
                                              threads, reps))
+
+    def build_continuum(self, dist: int, names: list[bytes], weights: list[int]) -> tuple[np.ndarray, np.ndarray]:
+        """The reference's own ketama_update (dist 0) / modula_update (1) over
+        all-live servers (oracle/ref_driver.c ref_build_continuum)."""
+        n = len(names)
+        cap = 160 * n * n + sum(weights) + 16
+        vals = np.zeros(cap, dtype=np.uint32)
+        idx = np.zeros(cap, dtype=np.uint32)
+        f = self.lib.ref_build_continuum
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint32),
+                      ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                      ctypes.c_uint32]
+        cnt = f(dist, (ctypes.c_char_p * n)(*names), (ctypes.c_uint32 * n)(*map(len, names)),
+                (ctypes.c_uint32 * n)(*weights), n, vals.ctypes.data, idx.ctypes.data, cap)
+        assert cnt >= 0
+        return vals[:cnt], idx[:cnt]

@@ -183,3 +183,38 @@ def test_device_continuum_end_to_end(gpu, oracle):
     torch.cuda.synchronize()
     want = oracle.server_idx_batch(1, 0, vals, idx, len(names), b"{}", keys, off)
     np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want)
+
+
+@pytest.mark.parametrize("pipe", [0, 1 << 28, 1 << 29], ids=["policy", "ring", "workgroup"])
+@pytest.mark.parametrize("tag", [b"::", b"()", b"$$", b"{}", b"ab", b"\x00\x01"], ids=["colons", "parens", "dollars",
+                                                                                      "braces", "ab", "nul01"])
+def test_hash_tag_neighbour_bytes(gpu, oracle, dist_fixture, tag, pipe):
+    """hash_tag trimming on keys built from the tag bytes and their +-1
+    neighbours (c ^ 1 next to c0 / c1: the bytes where a borrowing zero-byte
+    test flags a false match, ADVICE r02 — ':;ab:' under '::', ')((x)' under
+    '()'), against the oracle's byte loop (src/nc_server.c:665-677)."""
+    import torch
+
+    from twemproxy_amd import _lib as L
+
+    c0, c1 = tag[0], tag[1]
+    alpha = sorted({c0, c1, c0 ^ 1, c1 ^ 1, (c0 + 1) & 255, (c1 - 1) & 255, ord("a"), ord("x")})
+    rng = np.random.default_rng(c0 * 256 + c1)
+    keyset = [b":;ab:", b")((x)", b"$%$", b"{|}", b"::", b":;:", b";:;:", b"(()", b"()(x)"]
+    keyset += [bytes(rng.choice(alpha, size=int(rng.integers(0, 24))).astype(np.uint8)) for _ in range(6000)]
+    keys, off = t.pack_keys(keyset)
+    kd, od = to_dev(keys, off, shift=1)
+    L.lib().nc_gpuhash_set_tuning(0, 0, pipe)
+    try:
+        for p, nserver in pools(dist_fixture):
+            kvals = np.array(p["ketama"]["values"], np.uint32)
+            kidx = np.array(p["ketama"]["indices"], np.uint32)
+            cd = t.continuum_device(kidx, kvals)
+            for m in (1, 3, 6, 10):
+                got = t.server_idx_device(m, "ketama", kd, od, cd, nserver, hash_tag=tag)
+                torch.cuda.synchronize()
+                want = oracle.server_idx_batch(m, 0, kvals, kidx, nserver, tag, keys, off)
+                np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want,
+                                              err_msg=f"tag={tag} {t.HASH_NAMES[m]} nserver={nserver}")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)

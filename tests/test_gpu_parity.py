@@ -430,3 +430,26 @@ def test_md5_fixed_length_specialisation(gpu, oracle, fl):
                                               err_msg=f"fl={fl} n={n} var={var}")
             finally:
                 L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
+@pytest.mark.parametrize("var", [1 << 24, (1 << 24) | (1 << 20)], ids=["wsort8", "wsort4"])
+def test_wsort_round_of_long_keys(gpu, oracle, var):
+    """A sorted round made only of class-63 keys (63+ bytes, unordered within
+    the class): tiles of 192 short keys plus 64 keys of 63-90 bytes, which
+    fit the 6 KiB slab, so the fourth round's shortest key is not at lane 0
+    (Lmin must be a wave minimum there), against the oracle."""
+    rng = np.random.default_rng(63)
+    parts = []
+    for _ in range(48):  # 48 tiles of 256 keys
+        lens = np.concatenate([rng.integers(0, 8, size=192), rng.integers(63, 91, size=64)])
+        rng.shuffle(lens)
+        parts += [rng.integers(0, 256, size=int(ln), dtype=np.uint8).tobytes() for ln in lens]
+    keys, off = t.pack_keys(parts)
+    kd, od = to_dev(keys, off, shift=9)
+    L.lib().nc_gpuhash_set_tuning(0, 0, var)
+    try:
+        for m in (0, 5, 6, 7, 8):
+            np.testing.assert_array_equal(gpu_hash(m, kd, od), oracle.batch(m, keys, off),
+                                          err_msg=f"var={var} mode={t.HASH_NAMES[m]}")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)

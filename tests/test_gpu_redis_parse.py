@@ -148,7 +148,9 @@ def test_limits(gpu, oracle):
         torch.cuda.synchronize()
         assert info["nkeys"] == 4 and info["first_error"] == 4 and info["nreqs"] == 5, info
         assert info["consumed"] == 4 * len(get)
-        assert status.cpu().tolist() == [0, 0, 0, 0]
+        # the failing request has a status slot too (max_reqs + 1 entries)
+        assert len(status) == info["nreqs"]
+        assert status.cpu().tolist() == [0, 0, 0, 0, -1]  # NC_GPUHASH_REDIS_EINVAL
         _, _, _, oi = oracle.redis_parse(get * 4 + b"x")[1:]
         assert (oi["nkeys"], oi["first_error"], oi["consumed"]) == (4, 4, 4 * len(get)), oi
 

@@ -549,12 +549,16 @@ struct WrDist {
 /* hash_tag trimming of server_pool_idx (src/nc_server.c:665-677): the first
  * c0, then the first c1 after it; with at least one byte between them the
  * key becomes the bytes in between. Four bytes at a time: a byte equal to c
- * is a zero byte of w ^ c*0x01010101, found with the carry-free zero-byte
- * test (x - 0x01010101) & ~x & 0x80808080, whose lowest set bit is exact
- * (borrows only reach bytes above a true zero), then v_ffbl. */
+ * is a zero byte of w ^ c*0x01010101, found with the exact zero-byte test
+ * ~(((x & 0x7f7f7f7f) + 0x7f7f7f7f) | x) & 0x80808080 (no carry leaves a
+ * byte, so EVERY set bit is a zero byte), then v_ffbl. The cheaper
+ * (x - 0x01010101) & ~x test is exact only in its lowest set bit: a borrow
+ * out of a true zero flags a 0x01 byte above it, and c1 is searched after
+ * masking off the bytes up to c0, where that lowest bit may be gone (tag
+ * "::" on key ":;ab:"). */
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x)
 {
-    return (x - 0x01010101u) & ~x & 0x80808080u;
+    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
 }
 
 template <class Src>

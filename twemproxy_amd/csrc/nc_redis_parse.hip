@@ -568,7 +568,7 @@ extern "C" rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps
         }
         /* the synthetic failing request after an ok chain holds no key: it is
          * reported in nreqs but does not count against max_reqs (its status
-         * is written only where d_req_status has room, below) */
+         * takes d_req_status's extra slot, index max_reqs at most) */
         if (e == hipSuccess && nreq - (bad_start ? 1u : 0u) > ps->max_reqs) {
             errno = ENOMEM;
             return NC_ENOMEM;
@@ -584,7 +584,7 @@ extern "C" rstatus_t nc_gpuhash_redis_parse_device(nc_gpuhash_redis_parser_t *ps
         if (e == hipSuccess && nreq) {
             hipLaunchKernelGGL(rd_req_kernel, dim3(grid_of(nm)), dim3(256), 0, st, ps->req, (uint32_t)(nreq < nm ? nreq : nm),
                                ps->cstatus, ps->cnk, ps->nk, d_req_status);
-            if (bad_start && d_req_status && nm < ps->max_reqs)
+            if (bad_start && d_req_status)
                 hipLaunchKernelGGL(rd_bad_start_kernel, dim3(1), dim3(1), 0, st, d_req_status, nm);
             e = hipGetLastError();
             /* nk[first_bad] = 0 so the exclusive scan's last element is the key total */

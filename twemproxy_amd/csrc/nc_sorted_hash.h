@@ -138,6 +138,17 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
+/* minimum over the wave's 64 lanes (uniform result) */
+__device__ __forceinline__ uint32_t wave_min(uint32_t v)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)v, d);
+        v = v < y ? v : y;
+    }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
 } // namespace nc_sh
 
 #endif

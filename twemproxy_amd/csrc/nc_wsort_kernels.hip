@@ -44,6 +44,7 @@ using nc_sh::hash_slab;
 using nc_sh::init_state;
 using nc_sh::wave_excl_scan;
 using nc_sh::wave_max;
+using nc_sh::wave_min;
 
 constexpr uint32_t kTK = 256;                 /* keys per tile (one wave) */
 constexpr uint32_t kJ = 6;                    /* 16-byte slab chunks per lane */
@@ -239,11 +240,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
             for (int r = 0; r < 4; r++) {
                 const uint32_t e = L.ent[64u * r + lane];
                 const uint32_t len = e >> 16;
-                /* ascending by class within the round: lane 0 the shortest;
-                 * lane 63 the longest unless the round reaches the last
-                 * class (63+), whose lengths are unordered */
-                const uint32_t lmin = (uint32_t)__builtin_amdgcn_readlane((int)len, 0);
+                /* ascending by class within the round: lane 0 the shortest
+                 * and lane 63 the longest, unless that lane's key is in the
+                 * last class (63+), whose lengths are unordered: then a wave
+                 * reduction */
+                uint32_t lmin = (uint32_t)__builtin_amdgcn_readlane((int)len, 0);
                 uint32_t lmax = (uint32_t)__builtin_amdgcn_readlane((int)len, 63);
+                if (lmin >= kClasses - 1u) lmin = wave_min(len);
                 if (lmax >= kClasses - 1u) lmax = wave_max(len);
                 if constexpr (NOHASH) hq[r] = len;
                 else hq[r] = final_state<MODE>(hash_slab<MODE>(L.slab, e & 0xffffu, len, lmin, lmax));

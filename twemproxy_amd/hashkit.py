@@ -131,12 +131,15 @@ def pick_variant(hash_: int | str, nkeys: int, shape=None) -> int:
     return v
 
 
-def _check_batch(keys, offsets, key_end=None) -> None:
+def _check_batch(keys, offsets, key_end=None, stream=None) -> None:
     """Argument checks of the device-resident entry points: uint8 keys, int64
     offsets, both contiguous CUDA tensors, and a key buffer readable
     NC_GPUHASH_PAD bytes past offsets[-1] (the kernels' vector reads run up to
-    that far). `key_end` is offsets[-1] as the packer knows it; when it is None
-    the value is read back from the device (one synchronising copy)."""
+    that far). `key_end` is offsets[-1] as the packer knows it. When it is None
+    the value is read back from the device ON THE LAUNCH STREAM `stream`, so it
+    is ordered after whatever wrote the offsets there: one synchronising copy,
+    which makes the call block until that stream reaches it. Pass key_end to
+    keep the launch asynchronous."""
     import torch
 
     if keys.dtype != torch.uint8 or offsets.dtype != torch.int64:
@@ -150,7 +153,26 @@ def _check_batch(keys, offsets, key_end=None) -> None:
     if not (keys.is_cuda and offsets.is_cuda):
         raise ValueError("device entry points need CUDA (HIP) tensors")
     if offsets.numel() > 1 and key_end is None:
-        _check_key_room(keys.numel(), int(offsets[-1].item()))
+        _check_key_room(keys.numel(), _read_last(offsets, stream))
+
+
+def _torch_stream(stream, device):
+    """The torch stream object of a launch-stream argument (None = current)."""
+    import torch
+
+    if stream is None:
+        return torch.cuda.current_stream(device)
+    if isinstance(stream, int):
+        return torch.cuda.ExternalStream(stream, device=device)
+    return stream
+
+
+def _read_last(offsets, stream) -> int:
+    """offsets[-1] read back on the launch stream (ordered after its writers)."""
+    import torch
+
+    with torch.cuda.stream(_torch_stream(stream, offsets.device)):
+        return int(offsets[-1].item())
 
 
 def _check_key_room(nbytes: int, end: int) -> None:
@@ -175,7 +197,7 @@ def hash_batch_device(hash_: int | str, keys, offsets, out=None, stream=None, sh
 
     mode = mode_of(hash_)
     n = offsets.numel() - 1
-    _check_batch(keys, offsets, key_end)
+    _check_batch(keys, offsets, key_end, stream)
     if out is None:
         out = torch.empty(max(n, 0), dtype=torch.int32, device=keys.device)
     elif out.dtype != torch.int32 or not out.is_cuda or not out.is_contiguous() or out.numel() < n:
@@ -237,7 +259,7 @@ def server_idx_device(hash_: int | str, dist: int | str, keys, offsets, continuu
     n = offsets.numel() - 1
     if hash_tag is not None and len(hash_tag) != 2:
         raise ValueError("hash_tag is two bytes (conf_set_hash_tag)")
-    _check_batch(keys, offsets, key_end)
+    _check_batch(keys, offsets, key_end, stream)
     if continuum.dtype != torch.int32 or not continuum.is_cuda or not continuum.is_contiguous():
         raise ValueError("continuum must be a contiguous int32 CUDA tensor (continuum_device())")
     if out is None:
@@ -344,7 +366,8 @@ class RedisParser(McParser):
         keys = torch.empty(nbytes + L.NC_GPUHASH_PAD, dtype=torch.uint8, device=dev)
         off = torch.empty(self.max_keys + 1, dtype=torch.int64, device=dev)
         kreq = torch.empty(self.max_keys, dtype=torch.int32, device=dev)
-        status = torch.empty(self.max_reqs, dtype=torch.int32, device=dev)
+        # max_reqs + 1: a failing request after max_reqs ok ones has a status too
+        status = torch.empty(self.max_reqs + 1, dtype=torch.int32, device=dev)
         res = L.NcRedisResult()
         L.check(
             self._lib.nc_gpuhash_redis_parse_device(
