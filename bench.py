@@ -192,6 +192,48 @@ def read_ceiling(t, rf, buf):
     rf["frac_of_read_ceiling"] = round(rf["achieved"] / probe, 4)
 
 
+SHARD_DIGESTS = os.path.join(HERE, "tests", "golden", "shard_digests.json")
+_digests = None
+
+
+def _load_digests():
+    global _digests
+    if _digests is None:
+        try:
+            _digests = json.load(open(SHARD_DIGESTS))["configs"]
+        except (OSError, ValueError, KeyError):
+            _digests = {}
+
+
+def rank_parity(torch, cfg: str, mode: str, out, first: int, nk: int, n_per_rank: int, world: int, rank: int):
+    """This rank's outputs against the compiled reference's digest of its
+    shard (tests/golden/shard_digests.json, made by
+    tests/golden/make_shard_digests.py): "ok", "MISMATCH", or "unpinned"
+    when this run's sizes or N have no digest. Outside every timed region."""
+    import hashlib
+
+    _load_digests()
+    c = _digests.get(cfg)
+    if not c or c["n_per_rank"] != n_per_rank or str(world) not in c["N"]:
+        return "unpinned"
+    want = c["N"][str(world)][rank]
+    if want["keys"] != [first, first + nk] or mode not in want:
+        return "MISMATCH (key range)"
+    got = hashlib.sha256(out[:nk].cpu().numpy().tobytes()).hexdigest()
+    return "ok" if got == want[mode] else "MISMATCH"
+
+
+def gather_parity(torch, status: str, dist_on: bool) -> list:
+    """every rank's status, in rank order (on every rank)"""
+    if not dist_on:
+        return [status]
+    import torch.distributed as dist
+
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, status)
+    return out
+
+
 PROFILED_NKEYS = {"C2": 1 << 26, "C3": 1 << 26, "C4": 1 << 25}  # tools/pmc_run.py sizes
 RUN_NKEYS = dict(PROFILED_NKEYS)  # this run's nominal keys per GPU (--nkeys / --c4-nkeys)
 
@@ -363,6 +405,13 @@ def main():
     }
     if scatter:
         res["scatter"] = scatter
+    parity = {}
+
+    def check(cfg, mode, out_, first_, nk_, per_rank):
+        parity[f"{cfg}/{mode}"] = gather_parity(
+            torch, rank_parity(torch, cfg, mode, out_, first_, nk_, per_rank, world, rank), dist_on)
+
+    check("C2", "fnv1a_64", out, first, nk, n_local)
 
     if not args.no_extra:
         # ---- md5 on the same keys: HBM and VALU rooflines
@@ -372,6 +421,7 @@ def main():
         m["roofline_hbm"] = m.pop("roofline")
         m["roofline"] = valu_roofline(md5_ops(torch, off), m["kernel_ms"], ceiling)  # md5's binding ceiling
         res["md5"] = m
+        check("C2", "md5", out, first, nk, n_local)
         # ---- fused server_pool_idx: fnv1a_64 + ketama_dispatch over
         # a synthetic sorted continuum of 8 servers x 160 points (LDS-staged)
         rng = np.random.default_rng(9)
@@ -393,7 +443,7 @@ def main():
     if not args.no_extra:
         # ---- C3 shape: fnv1a_64 (the 70 % target), crc32 (+ its LDS traffic), md5
         c3 = t.CONFIGS["C3"]["spec"]
-        keys3, off3, _, sc3 = resident(c3, n_local)
+        keys3, off3, first3, sc3 = resident(c3, n_local)
         nk3 = off3.numel() - 1
         kb3 = int(off3[-1].item())
         out3 = torch.empty(nk3, dtype=torch.int32, device=dev)
@@ -402,6 +452,7 @@ def main():
                  f"C3: fnv1a_64 over {n_local} x 32 B keys per GPU", "C3")
         read_ceiling(t, f3["roofline"], keys3)
         res["c3_fnv1a_64"] = f3
+        check("C3", "fnv1a_64", out3, first3, nk3, n_local)
         c = leg(t, torch, "crc32", keys3, off3, out3, args.steps, args.warmup, dist_on, sh3, kb3, nk3, kb3,
                 f"C3: crc32 over {n_local} x 32 B keys per GPU", "C3")
         # slicing-by-4: 4 table lookups (4 B each) per 4 key bytes
@@ -411,11 +462,13 @@ def main():
                              "frac": round(lds_gbs / LDS_PEAK_GBS, 4), "lds_bytes_per_launch": int(lds_bytes),
                              "note": "table reads only: 1 ds_read_b32 per key byte, near conflict-free copies"}
         res["c3_crc32"] = c
+        check("C3", "crc32", out3, first3, nk3, n_local)
         m3 = leg(t, torch, "md5", keys3, off3, out3, max(5, args.steps // 2), 1, dist_on, sh3, kb3, nk3, kb3,
                  f"C3: md5 over {n_local} x 32 B keys per GPU", "C3")
         m3["roofline_hbm"] = m3.pop("roofline")
         m3["roofline"] = valu_roofline(md5_ops(torch, off3), m3["kernel_ms"], ceiling)
         res["c3_md5"] = m3
+        check("C3", "md5", out3, first3, nk3, n_local)
         if sc3:
             res["c3_scatter"] = sc3
         del keys3, off3, out3
@@ -425,7 +478,7 @@ def main():
         # ---- C4 shard: 256-byte keys, one GPU's share of configs[3] (scattered from rank 0 at N > 1)
         c4 = t.CONFIGS["C4"]["spec"]
         n4 = args.c4_nkeys
-        keys4, off4, _, sc4 = resident(c4, n4)
+        keys4, off4, first4, sc4 = resident(c4, n4)
         nk4 = off4.numel() - 1
         kb4 = int(off4[-1].item())
         out4 = torch.empty(nk4, dtype=torch.int32, device=dev)
@@ -437,6 +490,7 @@ def main():
             if mode == "md5":
                 x["roofline_valu"] = valu_roofline(md5_ops(torch, off4), x["kernel_ms"], ceiling)
             r4[mode] = x
+            check("C4", mode, out4, first4, nk4, n4)
         if sc4:
             r4["scatter"] = sc4
         res["c4_shard"] = r4
@@ -451,9 +505,38 @@ def main():
         except Exception as e:  # reported beside the headline, never instead of it
             res["redis_key_extraction"] = {"error": repr(e)}
 
+    # ---- end to end from pinned host memory (PCIe-inclusive; never `value`):
+    # the whole C2 batch on rank 0 at N = 1, and the §8e alternative ingest —
+    # every rank pulls its own C4 shard H2D from pinned host memory and hashes it
+    if not args.no_extra:
+        _load_digests()
+        if world == 1 and rank == 0:
+            try:
+                d2 = _digests.get("C2", {}).get("N", {}).get("1") if args.nkeys == 1 << 26 else None
+                res["e2e_c2"] = e2e_leg(t, torch, "C2", spec, 0, args.nkeys, "fnv1a_64", dev, d2[0] if d2 else None,
+                                        world, rank, dist_on)
+            except Exception as e:
+                res["e2e_c2"] = {"error": repr(e)}
+        if not args.no_c4:
+            try:
+                n4 = args.c4_nkeys
+                d4 = _digests.get("C4", {}).get("N", {}).get(str(world)) if n4 == 1 << 25 else None
+                res["c4_ingest"] = e2e_leg(t, torch, "C4 shard (per rank)", t.CONFIGS["C4"]["spec"], rank * n4, n4, "md5",
+                                           dev, d4[rank] if d4 else None, world, rank, dist_on,
+                                           chunk=(1 << 20, 1 << 28, 3))
+            except Exception as e:
+                res["c4_ingest"] = {"error": repr(e)}
+
     # ---- C5 pipelined GET replay through the host batch API (rank 0, N = 1)
     if rank == 0 and world == 1 and not args.no_extra:
         res["c5_e2e"] = c5_leg()
+
+    # ---- every rank's outputs against the reference's per-shard digests
+    flat = [v for st in parity.values() for v in st]
+    res["parity"] = {"all": "ok" if flat and all(v == "ok" for v in flat) else
+                     ("unpinned" if all(v == "unpinned" for v in flat) else "FAIL"),
+                     "per_rank": parity,
+                     "source": "tests/golden/shard_digests.json (sha256 of the compiled reference's outputs per rank)"}
 
     # ---- CPU baseline (rank 0, N = 1)
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -468,6 +551,81 @@ def main():
 
         dist.barrier()
         dist.destroy_process_group()
+
+
+def h2d_probe(torch, src, dev, reps=3):
+    """Same-run PCIe H2D ceiling: GB/s of one hipMemcpyAsync of the pinned
+    host tensor `src` into device memory (best of `reps`)."""
+    dst = torch.empty(src.numel(), dtype=src.dtype, device=dev)
+    best = None
+    for _ in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dst.copy_(src, non_blocking=True)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del dst
+    return src.numel() * src.element_size() / (best * 1e-3) / 1e9
+
+
+def pinned_copy(torch, x):
+    h = torch.empty(x.numel(), dtype=x.dtype).pin_memory()
+    h.copy_(x)
+    return h
+
+
+def e2e_leg(t, torch, cfg, spec, first, n, mode, dev, digest_rank, world, rank, dist_on, reps=3,
+            chunk=(1 << 22, 1 << 26, 3)):
+    """End to end from a host CSR in pinned memory: chunked
+    H2D -> kernel -> D2H over the whole batch (nc_gpuhash_batch_pinned, three
+    streams), the caller's buffers used in place. The inputs are generated on
+    the device and copied into pinned host tensors before any timing; the
+    outputs land in pinned host memory and are checked against the compiled
+    reference's digest. Beside it the same run's H2D ceiling (one large
+    hipMemcpyAsync)."""
+    import hashlib
+
+    kd, od = t.synth_device(spec, first, n, device=dev)
+    kb = int(od[-1].item())
+    keys_h = pinned_copy(torch, kd)
+    off_h = pinned_copy(torch, od)
+    out_h = torch.empty(n, dtype=torch.int32).pin_memory()
+    del kd, od
+    torch.cuda.empty_cache()
+    probe = h2d_probe(torch, keys_h, dev)
+    h2d_bytes = kb + 8 * (n + 1)
+    shape = spec.shape(kb)
+    res = {"workload": f"{cfg}: {n} keys ({kb} key bytes) in pinned host memory -> {mode} -> hashes in pinned "
+                       f"host memory", "h2d_bytes": h2d_bytes, "d2h_bytes": 4 * n,
+           "h2d_probe_gbs": round(probe, 2),
+           "chunk": {"keys": chunk[0], "bytes": chunk[1], "depth": chunk[2]}}
+    with t.Pipe(torch.cuda.current_device(), *chunk) as p:
+        try:
+            p.hash(mode, keys_h, off_h, out_h, shape=shape)  # warm-up
+            if dist_on:
+                import torch.distributed as dist
+
+                dist.barrier()
+            best = None
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                p.hash(mode, keys_h, off_h, out_h, shape=shape)
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            wall = max_over_ranks(torch, best, dist_on)
+            got = hashlib.sha256(out_h.numpy().tobytes()).hexdigest()
+            res.update({"ms": round(wall * 1e3, 2),
+                        "value": round(sum_over_ranks(torch, float(n), dist_on) / wall / 1e6, 1), "unit": "Mkeys/s",
+                        "h2d_gbs": round(h2d_bytes / best / 1e9, 2),
+                        "frac_of_h2d_probe": round(h2d_bytes / best / 1e9 / probe, 4),
+                        "parity": "ok" if digest_rank and got == digest_rank.get(mode) else
+                                  ("unpinned" if not digest_rank else "MISMATCH")})
+        except Exception as e:  # reported beside the headline, never instead of it
+            res["error"] = repr(e)
+    del keys_h, off_h, out_h
+    return res
 
 
 def c5_leg(seconds=0.4):

@@ -272,6 +272,34 @@ rstatus_t nc_gpuhash_wait(nc_gpuhash_ctx_t *ctx, int ticket);
 rstatus_t nc_hashkit_batch(int mode, const uint8_t *keys, const uint64_t *offsets,
                            uint32_t nkeys, uint32_t *out);
 
+/* ---- 3c. whole host batches from caller-pinned memory (no repack) ----
+ * The large-batch host path (SURVEY.md §8d end to end: host CSR (pinned) ->
+ * hipMemcpyAsync H2D -> kernel -> D2H). The caller's CSR is used where it
+ * lies: memory from hipHostMalloc, or registered once with
+ * nc_gpuhash_host_register (a proxy pins its mbuf arena). A pipe holds
+ * `depth` device chunk buffers and three streams (H2D, kernel, D2H): chunk
+ * i+1's keys and offsets go up while chunk i hashes and chunk i-1's hashes
+ * come back. Chunks are contiguous key ranges of at most chunk_keys keys and
+ * chunk_bytes key bytes. */
+typedef struct nc_gpuhash_pipe nc_gpuhash_pipe_t;
+
+nc_gpuhash_pipe_t *nc_gpuhash_pipe_create(int device, uint64_t chunk_keys, uint64_t chunk_bytes, int depth);
+void nc_gpuhash_pipe_destroy(nc_gpuhash_pipe_t *p);
+
+/* Hash keys [0, nkeys) of a pinned host CSR into the pinned `out`; blocks
+ * until every hash is in `out`. keys must be readable NC_GPUHASH_PAD bytes
+ * past offsets[nkeys] (the device contract); shape may be NULL. A key longer
+ * than chunk_bytes is NC_ENOMEM. Not thread-safe per pipe (one batch at a
+ * time; use a pipe per thread). flags: 0 (reserved). */
+rstatus_t nc_gpuhash_batch_pinned(nc_gpuhash_pipe_t *p, int mode, const uint8_t *keys, const uint64_t *offsets,
+                                  uint64_t nkeys, uint32_t *out, const struct nc_gpuhash_shape *shape,
+                                  int flags);
+
+/* Page-lock (and map) an existing host range for the pinned path
+ * (hipHostRegister), and undo it. */
+rstatus_t nc_gpuhash_host_register(void *ptr, size_t bytes);
+rstatus_t nc_gpuhash_host_unregister(void *ptr);
+
 /* ---- 4. multi-GPU shard planning ----
  * Split keys [0, nkeys) into nshards contiguous ranges with about equal key
  * bytes: key_bounds[g] .. key_bounds[g+1] is shard g (nshards + 1 entries). */

@@ -65,8 +65,10 @@ rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const u
  * 20-23 its options (tiles per wave, 128-byte line image, grid interleave);
  * bit 24: the wave-sorted pipeline (fnv x4, one_at_a_time), bits 20-21 its
  * tiles per wave, bit 22 DIAGNOSTIC no-hash build (fnv1a_64), bit 23 its
- * tiles interleaved over the grid; bit 26: md5 without its fixed-length
- * specialisation (A/B); -1 = keep). */
+ * tiles interleaved over the grid; bit 25: the grouped workgroup pipeline
+ * (each wave one length quartile of the tile), bit 20 its DIAGNOSTIC no-hash
+ * build (fnv1a_64), bits 21-22 its resident sets (6, 1, 3, 8); bit 26: md5
+ * without its fixed-length specialisation (A/B); -1 = keep). */
 rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
 #ifdef __cplusplus

@@ -138,19 +138,21 @@ def test_auto_policy_choices():
     for both); the register-staged workgroup pipeline when the
     shape is unknown; oversubscribed workgroup grids (and length grouping) for
     varying lengths; the wave ring for fixed 20-40 B fnv-like keys; the
-    wave-sorted pipeline for one_at_a_time on C2-like shapes."""
+    grouped workgroup pipeline (one length quartile per wave) on C2-like
+    shapes."""
     WG, RS, RING5, RING4 = 1 << 16, 32, 128 | (3 << 8), 128
     SORTED, OVER = 1 << 17, 1 << 18
     DIRECT, DIRECT_LDS, IL32 = 1 << 19, 4 << 20, (8 | 2) << 20
-    WSORT = 1 << 24
+    WSORT, GSORT = 1 << 24, 1 << 25
     n = 1 << 26
     assert t.pick_variant("fnv1a_64", n) == RS
     assert t.pick_variant("md5", n) == DIRECT  # unknown shape
     # C2 (Zipf 8-64 B, mean 19.3)
-    assert t.pick_variant("fnv1a_64", n, (19 * n, 8, 64)) == WG | OVER
+    for name in ("fnv1a_64", "fnv1_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur", "jenkins", "crc16"):
+        assert t.pick_variant(name, n, (19 * n, 8, 64)) == GSORT, name
     assert t.pick_variant("crc32", n, (19 * n, 8, 64)) == WG | OVER
-    assert t.pick_variant("one_at_a_time", n, (19 * n, 8, 64)) == WSORT
-    assert t.pick_variant("one_at_a_time", n, (21 * n, 8, 64)) == WG | SORTED | OVER
+    assert t.pick_variant("one_at_a_time", n, (19 * n, 8, 64)) == GSORT | (2 << 21)
+    assert t.pick_variant("one_at_a_time", n, (21 * n, 8, 64)) == GSORT | (2 << 21)
     assert t.pick_variant("md5", n, (19 * n, 8, 64)) == DIRECT
     # uniform 8-64 B (mean 36)
     assert t.pick_variant("fnv1a_64", n, (36 * n, 8, 64)) == RS

@@ -131,3 +131,52 @@ def test_context_shared_by_worker_threads(gpu, oracle):
             th.join(120)
         assert not any(th.is_alive() for th in threads)
     assert errors == []
+
+
+@pytest.mark.parametrize("chunk", [(1000, 1 << 14, 2), (4096, 1 << 16, 3), (1 << 20, 1 << 24, 4)],
+                         ids=["tiny2", "small3", "big4"])
+def test_pinned_pipe_matches_oracle(gpu, oracle, chunk):
+    """nc_gpuhash_batch_pinned over torch-pinned host CSRs: many chunks
+    (keys cut by the key and byte limits), mixed lengths incl. empty and long
+    keys, every mode, against the oracle."""
+    import torch
+
+    ck, cb, depth = chunk
+    keys_np, off_np = t.synth_host(t.SynthSpec.uniform(77, 0, 700), 0, 30001)
+    keys = torch.from_numpy(keys_np).pin_memory()
+    off = torch.from_numpy(off_np.astype(np.int64)).pin_memory()
+    out = torch.empty(30001, dtype=torch.int32).pin_memory()
+    with t.Pipe(0, ck, cb, depth) as p:
+        for m in range(12):
+            want = oracle.batch(m, keys_np, off_np)
+            out.fill_(0)
+            p.hash(m, keys, off, out, shape=t.shape_of(off_np))
+            np.testing.assert_array_equal(out.numpy().view(np.uint32), want,
+                                          err_msg=f"mode {t.HASH_NAMES[m]} chunk={chunk}")
+
+
+def test_pinned_pipe_registered_numpy_and_limits(gpu, oracle):
+    """host_register'ed numpy buffers (a proxy pinning its mbuf arena), a
+    batch whose offsets do not start at 0, and a key longer than a chunk."""
+    import torch
+
+    keys_np, off_np = t.synth_host(t.CONFIGS["C2"]["spec"], 5, 50000)
+    off_np = off_np + np.uint64(0)  # own copy
+    out = np.zeros(50000 - 7, dtype=np.uint32)
+    for a in (keys_np, off_np, out):
+        t.host_register(a.ctypes.data, a.nbytes)
+    try:
+        with t.Pipe(0, 1 << 12, 1 << 15, 2) as p:
+            sub = off_np[7:]  # offsets[0] != 0
+            p.hash("fnv1a_64", keys_np.ctypes.data, sub.ctypes.data, out.ctypes.data, nkeys=sub.size - 1)
+            np.testing.assert_array_equal(out, oracle.batch(6, keys_np, off_np)[7:])
+        big, boff = t.pack_keys([b"x" * 5000])
+        with t.Pipe(0, 16, 4096, 2) as p:
+            bk = torch.from_numpy(big).pin_memory()
+            bo = torch.from_numpy(boff.astype(np.int64)).pin_memory()
+            bout = torch.empty(1, dtype=torch.int32).pin_memory()
+            with pytest.raises(t.NcError):
+                p.hash("md5", bk, bo, bout)
+    finally:
+        for a in (keys_np, off_np, out):
+            t.host_unregister(a.ctypes.data)

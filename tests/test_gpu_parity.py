@@ -43,7 +43,8 @@ def gpu_hash(mode, keys_d, off_d):
                         (0, 0, 10624), (0, 0, 16512), (7, 0, 16512 | 2048 | 768), (0, 0, 16512 | 1792),
                         (0, 0, 65536 | (1 << 18)), (0, 1, 32 | (1 << 18)), (0, 0, 1 << 19),
                         (0, 0, (1 << 19) | (4 << 20)), (0, 0, (1 << 19) | (10 << 20)),
-                        (0, 0, (1 << 19) | (14 << 20)), (0, 0, 1 << 24), (0, 0, (1 << 24) | (9 << 20))],
+                        (0, 0, (1 << 19) | (14 << 20)), (0, 0, 1 << 24), (0, 0, (1 << 24) | (9 << 20)),
+                        (0, 0, 1 << 25), (37, 0, 1 << 25), (0, 0, (1 << 25) | (1 << 21))],
                 ids=["persistent+sort", "auto", "workgroup", "grid37+sort+shiftadd", "shiftadd", "grid5+sort",
                      "sorted_bit", "regstage", "regstage+sort", "grid11+regstage+sort+shiftadd", "grid9+regstage",
                      "cached", "cached+sort", "regstage+cached", "grid7+regstage+cached+sort", "wavering",
@@ -51,7 +52,8 @@ def gpu_hash(mode, keys_d, off_d):
                      "wavering+cached", "wavering_w4_pair", "grid3+wavering_3_1_2_w4_pair", "wavering_w4",
                      "wavering_t64_w4", "wavering_t256_sorted", "grid7+wavering_t256_sorted_w4_6_2_3",
                      "wavering_t256_sorted_5_1_2", "workgroup_over3", "regstage+sort+over3", "direct",
-                     "direct_lines", "direct_il32", "direct_lines_il32", "wsort", "wsort_il4"])
+                     "direct_lines", "direct_il32", "direct_lines_il32", "wsort", "wsort_il4",
+                     "gsort", "grid37+gsort", "gsort_1set"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)
@@ -237,7 +239,8 @@ def test_sort_and_grid_variants_agree_full_size(gpu):
                             (0, 1, 65536), (3, 1, 1), (0, 0, 1 << 17), (7, 0, 2176), (0, 0, 32), (0, 1, 32), (5, 1, 33), (13, 1, 32), (1024, 0, 32),
                             (1536, 0, 32), (2048, 1, 32), (0, 0, 64), (0, 1, 64), (0, 0, 96), (1536, 1, 96),
                             (0, 0, 128), (1, 0, 128), (7, 0, 384), (0, 0, 640), (2048, 0, 896), (0, 0, 129),
-                            (0, 0, 192), (0, 0, 1 << 24), (0, 0, (1 << 24) | (2 << 20)), (0, 0, (1 << 24) | (8 << 20))):
+                            (0, 0, 192), (0, 0, 1 << 24), (0, 0, (1 << 24) | (2 << 20)), (0, 0, (1 << 24) | (8 << 20)),
+                            (0, 0, 1 << 25), (1, 0, 1 << 25), (4096, 0, 1 << 25), (0, 0, (1 << 25) | (3 << 21))):
         L.lib().nc_gpuhash_set_tuning(grid, sort, var)
         out = t.hash_batch_device("fnv1a_64", kd, od)
         torch.cuda.synchronize()
@@ -264,7 +267,7 @@ def test_key_buffers_beyond_4gib(gpu):
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     try:
         for var in (0, 65536, 32, 128, 896, 2176, 1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (14 << 20),
-                    (1 << 19) | (8 << 20), 1 << 24):
+                    (1 << 19) | (8 << 20), 1 << 24, 1 << 25):
             L.lib().nc_gpuhash_set_tuning(0, 0, var)
             for name in ("md5", "crc32", "fnv1a_64"):
                 t.hash_batch_device(name, kd, od, out, shape=spec.shape(256 * n))
@@ -453,3 +456,67 @@ def test_wsort_round_of_long_keys(gpu, oracle, var):
                                           err_msg=f"var={var} mode={t.HASH_NAMES[m]}")
     finally:
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
+@pytest.mark.parametrize("tune", [(0, 1 << 25), (0, (1 << 25) | (1 << 21)), (3, 1 << 25), (1, (1 << 25) | (3 << 21))],
+                         ids=["gsort6", "gsort1", "grid3", "grid1_8sets"])
+def test_gsort_ragged_tiles(gpu, oracle, tune):
+    """The grouped workgroup pipeline (variant bit 25: offsets by LDS-DMA two
+    tiles ahead, wave 0 sorting the next tile, each wave one length quartile)
+    on batch sizes around its 256-key tile, empty keys, Zipf / uniform /
+    fixed lengths, tiles whose slab overflows its 6 KiB buffer (the global
+    path, alone and mixed), a misaligned key buffer and offsets not starting
+    at 0, every mode, against the oracle."""
+    grid, var = tune
+    L.lib().nc_gpuhash_set_tuning(grid, 0, var)
+    try:
+        for n, spec in ((1, t.SynthSpec.uniform(80, 0, 3)), (2, t.SynthSpec.fixed(81, 0)), (63, t.SynthSpec.zipf(82)),
+                        (255, t.SynthSpec.zipf(83)), (256, t.SynthSpec.fixed(84, 24)),
+                        (257, t.SynthSpec.uniform(85, 0, 64)), (513, t.SynthSpec.zipf(86)),
+                        (4097, t.SynthSpec.zipf(87)), (9000, t.SynthSpec.uniform(88, 0, 60)),
+                        (70001, t.SynthSpec.zipf(89)), (3000, t.SynthSpec.uniform(90, 0, 300)),
+                        (600, t.SynthSpec.uniform(91, 0, 2000)), (2049, t.SynthSpec.fixed(92, 25))):
+            keys, off = t.synth_host(spec, 3, n)
+            kd, od = to_dev(keys, off, shift=5)
+            for m in MODES:
+                np.testing.assert_array_equal(gpu_hash(m, kd, od), oracle.batch(m, keys, off),
+                                              err_msg=f"tune={tune} n={n} spec={spec} mode={t.HASH_NAMES[m]}")
+            if n > 1:  # a sub-batch whose offsets do not start at 0
+                kd2, od2 = kd, od[1:].contiguous()
+                np.testing.assert_array_equal(gpu_hash(6, kd2, od2), oracle.batch(6, keys, off)[1:],
+                                              err_msg=f"tune={tune} n={n} offset base")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
+def test_virtual_key_base(gpu, oracle):
+    """A batch whose offsets start far from 0 and whose key pointer is
+    therefore not itself readable (keys - offsets[0] of a chunk of a larger
+    CSR, as nc_gpuhash_batch_pinned hands its chunks to the kernels): every
+    pipeline must only touch bytes inside [keys + offsets[0], keys +
+    offsets[n] + NC_GPUHASH_PAD). The base is moved 1 TiB below the buffer."""
+    import ctypes
+
+    import torch
+
+    shift = 1 << 40
+    for n, spec in ((3000, t.SynthSpec.uniform(93, 0, 700)), (5000, t.SynthSpec.zipf(94)),
+                    (4096, t.SynthSpec.fixed(95, 32)), (300, t.SynthSpec.fixed(96, 256))):
+        keys, off = t.synth_host(spec, 0, n)
+        kd = torch.from_numpy(keys).cuda()
+        od = torch.from_numpy(off.astype(np.int64) + shift).cuda()
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        shape = L.NcShape(int(off[-1]), *spec.len_range())
+        for var in (0, 65536, 32, 128, 896, 1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (14 << 20), 1 << 24,
+                    1 << 25):
+            L.lib().nc_gpuhash_set_tuning(0, 0, var)
+            try:
+                for m in MODES:
+                    L.check(L.lib().nc_gpuhash_batch_device_shaped(m, kd.data_ptr() - shift, od.data_ptr(), n,
+                                                                  out.data_ptr(), ctypes.byref(shape), None),
+                            "nc_gpuhash_batch_device_shaped")
+                    torch.cuda.synchronize()
+                    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), oracle.batch(m, keys, off),
+                                                  err_msg=f"var={var} n={n} mode={t.HASH_NAMES[m]}")
+            finally:
+                L.lib().nc_gpuhash_set_tuning(0, 0, 0)

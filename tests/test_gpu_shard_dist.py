@@ -68,3 +68,57 @@ def test_shards_hashed_by_the_kernel(gpu, spec_args, n):
         assert p.exitcode == 0
     assert all(r[1] for r in res), res
     assert res[0][2] == 0 and res[0][3] + res[1][3] == n and res[1][2] == res[0][3]
+
+
+def _shard_setup(cfg: str, modes):
+    """Rank 0's N = 8 set-up of bench.py --gpus 8 on one GPU: the whole
+    8 x n_per_rank batch of `cfg` generated on the device (C4: 2^28 x 256 B =
+    64 GiB + 2 GiB of offsets), plan_bounds, then every rank's shard cut and
+    copied the way scatter_shards hands it over (shard_of, the root's local
+    copy, offsets rebased to 0), hashed with the shape the bench passes,
+    against the compiled reference's per-rank digests
+    (tests/golden/shard_digests.json)."""
+    import hashlib
+    import json
+
+    import torch
+
+    from twemproxy_amd.shard import plan_bounds, shard_of
+
+    dg = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "shard_digests.json")))["configs"][cfg]
+    spec = t.CONFIGS[cfg]["spec"]
+    world = 8
+    fk, fo = t.synth_device(spec, 0, dg["n_per_rank"] * world)
+    kb = plan_bounds(fo, world)
+    bb = fo[kb]
+    kb, bb = kb.tolist(), bb.tolist()
+    assert [[kb[r], kb[r + 1]] for r in range(world)] == [x["keys"] for x in dg["N"]["8"]]
+    assert [[bb[r], bb[r + 1]] for r in range(world)] == [x["bytes"] for x in dg["N"]["8"]]
+    for r in range(world):
+        ks, os_ = shard_of(fk, fo, kb, bb, r)
+        lk = torch.zeros(ks.numel() + t.NC_GPUHASH_PAD, dtype=torch.uint8, device="cuda")
+        lk[: ks.numel()].copy_(ks)
+        lo = os_ - bb[r]
+        nk = lo.numel() - 1
+        out = torch.empty(nk, dtype=torch.int32, device="cuda")
+        shape = spec.shape(ks.numel())
+        for mode in modes:
+            t.hash_batch_device(mode, lk, lo, out, shape=shape, key_end=ks.numel())
+            torch.cuda.synchronize()
+            got = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()
+            assert got == dg["N"]["8"][r][mode], (cfg, mode, r)
+        del lk, lo, out
+    del fk, fo
+    torch.cuda.empty_cache()
+
+
+def test_shard_setup_n8_c4(gpu):
+    _shard_setup("C4", ("md5", "crc32", "fnv1a_64"))
+
+
+def test_shard_setup_n8_c2(gpu):
+    _shard_setup("C2", ("fnv1a_64", "md5"))
+
+
+def test_shard_setup_n8_c3(gpu):
+    _shard_setup("C3", ("fnv1a_64", "crc32", "md5"))

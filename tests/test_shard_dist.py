@@ -19,10 +19,14 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, spec_args, n, q):
+def _worker(rank, world, port, spec_args, n, q, msg=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        if msg:  # small message cap: every shard goes as many pieces
+            import twemproxy_amd.shard as sh
+
+            sh.MAX_MSG_BYTES = msg
         from tests.oracle_lib import Oracle
 
         spec = t.SynthSpec(*spec_args)
@@ -42,14 +46,15 @@ def _worker(rank, world, port, spec_args, n, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("msg", [None, 777], ids=["whole", "pieces777"])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("spec_args,n", [((2, t.hashkit.SYNTH_ZIPF, 8, 57), 20000),
                                          ((6, t.hashkit.SYNTH_UNIFORM, 0, 600), 3000)])
-def test_scatter_and_hash_shards(world, spec_args, n):
+def test_scatter_and_hash_shards(world, spec_args, n, msg):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, spec_args, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, spec_args, n, q, msg)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in range(world))

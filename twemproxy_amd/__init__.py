@@ -16,6 +16,7 @@ from .hashkit import (
     NMODES,
     Context,
     McParser,
+    Pipe,
     RedisParser,
     SynthSpec,
     conf_set_hash,
@@ -25,6 +26,8 @@ from .hashkit import (
     hash_batch_host,
     hash_key,
     hash_keys,
+    host_register,
+    host_unregister,
     ketama_hash,
     ketama_build_device,
     md5_signature,
@@ -45,5 +48,5 @@ __all__ = [
     "BYTES_FULL", "BYTES_PRINTABLE", "CONFIGS", "DIST_NAMES", "HASH_DEFAULT", "HASH_NAMES", "NMODES",
     "Context", "SynthSpec", "conf_set_hash", "device_count", "hash_batch_device", "hash_batch_host",
     "hash_key", "hash_keys", "ketama_hash", "md5_signature", "mode_of", "pack_keys", "pick_variant", "probe_read_gbs", "server_idx_device", "shape_of", "shard_bounds", "continuum_device", "ketama_build_device", "McParser", "RedisParser",
-    "synth_device", "synth_host", "time_batch_device",
+    "synth_device", "synth_host", "time_batch_device", "Pipe", "host_register", "host_unregister",
 ]

@@ -148,6 +148,16 @@ SIGNATURES = {
     "nc_hashkit_batch": (
         ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     ),
+    # whole batches from caller-pinned memory
+    "nc_gpuhash_pipe_create": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
+    "nc_gpuhash_pipe_destroy": (None, [ctypes.c_void_p]),
+    "nc_gpuhash_batch_pinned": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+         ctypes.POINTER(NcShape), ctypes.c_int],
+    ),
+    "nc_gpuhash_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "nc_gpuhash_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
     # sharding / info
     "nc_gpuhash_shard_bounds": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
     "nc_gpuhash_device_count": (ctypes.c_int, []),

@@ -16,6 +16,7 @@
  */
 #include <errno.h>
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -138,6 +139,7 @@ struct nc_gpuhash_ctx {
 
 static rstatus_t hip_fail(hipError_t e)
 {
+    if (getenv("NC_GPUHASH_DEBUG") != NULL) fprintf(stderr, "nc_gpuhash: host path: %s\n", hipGetErrorString(e));
     errno = (e == hipErrorNoDevice || e == hipErrorInvalidDevice) ? ENODEV
           : (e == hipErrorOutOfMemory ? ENOMEM : EIO);
     return errno == ENOMEM ? NC_ENOMEM : NC_ERROR;
@@ -474,4 +476,201 @@ rstatus_t nc_hashkit_batch(int mode, const uint8_t *keys, const uint64_t *offset
     if (rc == NC_OK) rc = nc_gpuhash_wait(g_ctx, ticket);
     pthread_mutex_unlock(&g_lock);
     return rc;
+}
+
+/* ---------------- whole batches from caller-pinned memory ---------------- */
+
+#define NC_PIPE_MAX_DEPTH 4
+
+struct nc_gpuhash_pipe {
+    int device;
+    int depth;
+    uint64_t chunk_keys, chunk_bytes;
+    hipStream_t s_h2d, s_comp, s_d2h;
+    uint8_t *d_keys[NC_PIPE_MAX_DEPTH];
+    uint64_t *d_off[NC_PIPE_MAX_DEPTH];
+    uint32_t *d_out[NC_PIPE_MAX_DEPTH];
+    hipEvent_t h2d_done[NC_PIPE_MAX_DEPTH], kern_done[NC_PIPE_MAX_DEPTH], d2h_done[NC_PIPE_MAX_DEPTH];
+};
+
+void nc_gpuhash_pipe_destroy(nc_gpuhash_pipe_t *p)
+{
+    if (p == NULL) return;
+    hipSetDevice(p->device);
+    if (p->s_h2d) hipStreamSynchronize(p->s_h2d);
+    if (p->s_comp) hipStreamSynchronize(p->s_comp);
+    if (p->s_d2h) hipStreamSynchronize(p->s_d2h);
+    for (int b = 0; b < NC_PIPE_MAX_DEPTH; b++) {
+        if (p->d_keys[b]) hipFree(p->d_keys[b]);
+        if (p->d_off[b]) hipFree(p->d_off[b]);
+        if (p->d_out[b]) hipFree(p->d_out[b]);
+        if (p->h2d_done[b]) hipEventDestroy(p->h2d_done[b]);
+        if (p->kern_done[b]) hipEventDestroy(p->kern_done[b]);
+        if (p->d2h_done[b]) hipEventDestroy(p->d2h_done[b]);
+    }
+    if (p->s_h2d) hipStreamDestroy(p->s_h2d);
+    if (p->s_comp) hipStreamDestroy(p->s_comp);
+    if (p->s_d2h) hipStreamDestroy(p->s_d2h);
+    free(p);
+}
+
+nc_gpuhash_pipe_t *nc_gpuhash_pipe_create(int device, uint64_t chunk_keys, uint64_t chunk_bytes, int depth)
+{
+    if (chunk_keys == 0 || chunk_bytes == 0 || depth < 2 || depth > NC_PIPE_MAX_DEPTH || chunk_keys >= (1ull << 32)) {
+        errno = EINVAL;
+        return NULL;
+    }
+    if (device < 0 || device >= nc_gpuhash_device_count()) {
+        errno = ENODEV;
+        return NULL;
+    }
+    nc_gpuhash_pipe_t *p = calloc(1, sizeof(*p));
+    if (p == NULL) {
+        errno = ENOMEM;
+        return NULL;
+    }
+    p->device = device;
+    p->depth = depth;
+    p->chunk_keys = chunk_keys;
+    p->chunk_bytes = chunk_bytes;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->s_h2d, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->s_comp, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->s_d2h, hipStreamNonBlocking);
+    for (int b = 0; b < depth && e == hipSuccess; b++) {
+        e = hipMalloc((void **)&p->d_keys[b], chunk_bytes + NC_GPUHASH_PAD);
+        if (e == hipSuccess) e = hipMalloc((void **)&p->d_off[b], (chunk_keys + 1) * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMalloc((void **)&p->d_out[b], chunk_keys * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&p->h2d_done[b], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&p->kern_done[b], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&p->d2h_done[b], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) {
+        hip_fail(e);
+        int saved = errno;
+        nc_gpuhash_pipe_destroy(p);
+        errno = saved;
+        return NULL;
+    }
+    return p;
+}
+
+/* last key index k1 > k0 such that keys [k0, k1) fit the chunk limits */
+static uint64_t pipe_cut(const nc_gpuhash_pipe_t *p, const uint64_t *off, uint64_t k0, uint64_t nkeys)
+{
+    uint64_t hi = nkeys - k0 < p->chunk_keys ? nkeys : k0 + p->chunk_keys;
+    const uint64_t limit = off[k0] + p->chunk_bytes;
+    if (off[hi] <= limit) return hi;
+    uint64_t lo = k0; /* largest k in [k0, hi) with off[k] <= limit */
+    while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (off[mid] <= limit) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+rstatus_t nc_gpuhash_batch_pinned(nc_gpuhash_pipe_t *p, int mode, const uint8_t *keys, const uint64_t *offsets,
+                                  uint64_t nkeys, uint32_t *out, const struct nc_gpuhash_shape *shape, int flags)
+{
+    if (p == NULL || offsets == NULL || (out == NULL && nkeys) || (keys == NULL && nkeys) || mode < 0 ||
+        mode >= NC_GPUHASH_NMODES) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    if (nkeys == 0) return NC_OK;
+    hipError_t e = hipSetDevice(p->device);
+    if (e != hipSuccess) return hip_fail(e);
+    if (flags != 0) { /* no flags are defined */
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    const char *dbgs = getenv("NC_GPUHASH_DEBUG");
+    const int dbg = dbgs ? atoi(dbgs) : 0;
+    uint64_t k0 = 0;
+    for (uint64_t c = 0; k0 < nkeys; c++) {
+        const int b = (int)(c % (uint64_t)p->depth);
+        const uint64_t k1 = pipe_cut(p, offsets, k0, nkeys);
+        if (k1 == k0) { /* one key longer than a chunk buffer */
+            hipStreamSynchronize(p->s_d2h);
+            errno = ENOMEM;
+            return NC_ENOMEM;
+        }
+        const uint64_t b0 = offsets[k0], nb = offsets[k1] - b0;
+        /* buffers of chunk c - depth: keys/offsets free once its kernel ran,
+         * out free once its hashes are back */
+        if (c >= (uint64_t)p->depth) e = hipStreamWaitEvent(p->s_h2d, p->kern_done[b], 0);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(p->d_keys[b], keys + b0, nb + NC_GPUHASH_PAD, hipMemcpyHostToDevice, p->s_h2d);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(p->d_off[b], offsets + k0, (k1 - k0 + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                               p->s_h2d);
+        if (e == hipSuccess) e = hipEventRecord(p->h2d_done[b], p->s_h2d);
+        if (e == hipSuccess) e = hipStreamWaitEvent(p->s_comp, p->h2d_done[b], 0);
+        if (e == hipSuccess && c >= (uint64_t)p->depth) e = hipStreamWaitEvent(p->s_comp, p->d2h_done[b], 0);
+        if (e != hipSuccess) break;
+        /* the chunk's offsets are absolute: hand the kernel the key base that
+         * puts offsets[k0] at the start of the chunk buffer */
+        struct nc_gpuhash_shape sh;
+        const struct nc_gpuhash_shape *shp = NULL;
+        if (shape != NULL) {
+            sh = *shape;
+            sh.key_bytes = nb;
+            shp = &sh;
+        }
+        if (dbg >= 2) { /* DIAGNOSTIC: each chunk's inputs checked on the host before its launch */
+            hipStreamSynchronize(p->s_h2d);
+            uint64_t o[2];
+            hipMemcpy(o, p->d_off[b], sizeof(o), hipMemcpyDeviceToHost);
+            uint64_t ol;
+            hipMemcpy(&ol, p->d_off[b] + (k1 - k0), sizeof(ol), hipMemcpyDeviceToHost);
+            fprintf(stderr, "nc_gpuhash pipe: mode %d chunk %llu buf %d keys [%llu, %llu) bytes [%llu, +%llu) dev off %llu %llu .. %llu%s\n",
+                    mode, (unsigned long long)c, b, (unsigned long long)k0, (unsigned long long)k1,
+                    (unsigned long long)b0, (unsigned long long)nb, (unsigned long long)o[0], (unsigned long long)o[1],
+                    (unsigned long long)ol, (o[0] != offsets[k0] || ol != offsets[k1]) ? " MISMATCH" : "");
+            if (o[0] != offsets[k0] || ol != offsets[k1]) {
+                errno = EIO;
+                return NC_ERROR;
+            }
+        }
+        if (nc_gpuhash_batch_device_shaped(mode, (const uint8_t *)((uintptr_t)p->d_keys[b] - b0), p->d_off[b], k1 - k0, p->d_out[b], shp,
+                                           p->s_comp) != NC_OK) {
+            hipStreamSynchronize(p->s_d2h);
+            return NC_ERROR;
+        }
+        if (dbg >= 2) {
+            e = hipStreamSynchronize(p->s_comp);
+            fprintf(stderr, "nc_gpuhash pipe: chunk %llu kernel: %s\n", (unsigned long long)c, hipGetErrorString(e));
+            if (e != hipSuccess) break;
+        }
+        e = hipEventRecord(p->kern_done[b], p->s_comp);
+        if (e == hipSuccess) e = hipStreamWaitEvent(p->s_d2h, p->kern_done[b], 0);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out + k0, p->d_out[b], (k1 - k0) * sizeof(uint32_t), hipMemcpyDeviceToHost, p->s_d2h);
+        if (e == hipSuccess) e = hipEventRecord(p->d2h_done[b], p->s_d2h);
+        if (e != hipSuccess) break;
+        k0 = k1;
+    }
+    hipError_t e2 = hipStreamSynchronize(p->s_d2h);
+    if (e == hipSuccess) e = e2;
+    return e == hipSuccess ? NC_OK : hip_fail(e);
+}
+
+rstatus_t nc_gpuhash_host_register(void *ptr, size_t bytes)
+{
+    if (ptr == NULL || bytes == 0) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterMapped);
+    return e == hipSuccess ? NC_OK : hip_fail(e);
+}
+
+rstatus_t nc_gpuhash_host_unregister(void *ptr)
+{
+    if (ptr == NULL) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    hipError_t e = hipHostUnregister(ptr);
+    return e == hipSuccess ? NC_OK : hip_fail(e);
 }

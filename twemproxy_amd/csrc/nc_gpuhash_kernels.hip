@@ -28,6 +28,7 @@
 
 #include <errno.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include "nc_gpuhash.h"
@@ -1028,6 +1029,200 @@ __global__ __launch_bounds__(kBlock, kMinWaves<MODE>()) void nc_hash_kernel(cons
     if (pend_idx != ~0ull) out[pend_idx] = pend_h;
 }
 
+/* ---------------- grouped workgroup pipeline (variant bit 25) ----------------
+ *
+ * The workgroup pipeline's tiles (256 keys, 4 waves, LDS-DMA slab double
+ * buffer, one barrier per tile), with each WAVE hashing one length quartile
+ * of the tile instead of 64 neighbouring keys: a wave runs as long as its
+ * longest key, so under Zipf 8-64 B four unsorted waves cost ~4 x 61 byte
+ * steps per tile, four length-grouped ones ~110. The grouping costs no
+ * barrier: a tile's offsets arrive by LDS-DMA two tiles ahead (the whole
+ * workgroup sees them after the top barrier), and wave 0 — which hashes the
+ * shortest quartile — counting-sorts tile t+1 while the others hash tile t,
+ * leaving the permutation in LDS for the next iteration. Offsets are read
+ * from HBM once, as 16-byte pieces (the plain pipeline reads each twice,
+ * 4 bytes per lane).
+ *
+ * Iteration t (after the top barrier: slab(t), offsets(t+1) and perm(t) are
+ * in LDS): pending stores of tile t-1; DMA offsets(t+2) and slab(t+1); wave 0
+ * sorts tile t+1; every wave hashes its quartile of tile t. */
+constexpr uint32_t kGsOffSlot = 2064;                  /* off[k0 .. k0+255] + end bound at [256], 16-aligned */
+constexpr uint32_t kGsCap = 6144;                      /* per slab buffer: Zipf 8-64 B tiles need ~5 KiB */
+constexpr uint32_t kGsOffs = 2 * kGsCap;               /* u64[3][258] */
+constexpr uint32_t kGsPerm = kGsOffs + 3 * kGsOffSlot; /* u8[2][256]: sorted position -> key index */
+constexpr uint32_t kGsHist = kGsPerm + 2 * kTile;      /* u32[64], the sorter's counters */
+constexpr uint32_t kGsTab = kGsHist + 4 * 64;          /* u32[256]: crc table / ketama bucket index */
+constexpr uint32_t kGsBytes = kGsTab + 4 * 256;
+static_assert(kGsBytes <= kLdsBudget, "8 workgroups per CU");
+static_assert(kGsOffs % 16 == 0 && kGsOffSlot % 16 == 0 && kGsTab % 16 == 0, "LDS carve must stay 16-byte aligned");
+
+__device__ __forceinline__ bool gs_fits(uint64_t span) { return span + 48u <= (uint64_t)kGsCap; }
+
+/* offsets of `tile` into slot: off[k0 .. k0+255] as 128 16-byte pieces (waves
+ * 0-1, pairs clamped inside off[0 .. nkeys]) and the end bound off[k0+cnt]
+ * at [256] (wave 2, two dwords) */
+template <int AUX>
+__device__ __forceinline__ void gs_issue_offs(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
+                                              uint8_t *slot, uint32_t t)
+{
+    const uint64_t k0 = tile * (uint64_t)kTile;
+    if (t < 128u) {
+        const uint64_t last_pair = (nkeys - 1u) & ~(uint64_t)1; /* off[p], off[p+1] stay <= nkeys */
+        uint64_t p = k0 + 2u * t;
+        if (p > last_pair) p = last_pair;
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)(off + p), (lds_void_t *)(slot + 16u * (t & ~63u)), 16, 0,
+                                         AUX);
+    } else if (t < 130u) {
+        const uint64_t e = k0 + tile_count(tile, nkeys);
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)(reinterpret_cast<const uint32_t *>(off + e) + (t - 128u)),
+                                         (lds_void_t *)(slot + 8u * kTile), 4, 0, AUX);
+    }
+}
+
+/* low dword of the start of key i (< cnt) and of its end, from an offsets slot */
+__device__ __forceinline__ uint32_t gs_lo(const uint8_t *slot, uint32_t i)
+{
+    return reinterpret_cast<const uint32_t *>(slot)[2u * i];
+}
+
+/* counting sort of the tile in `slot` by length class (one wave): perm[pos]
+ * = key index, ascending classes; absent keys (>= cnt) last (class 63; valid
+ * keys clamp to 62) */
+__device__ __forceinline__ void gs_sort(const uint8_t *slot, uint32_t cnt, uint32_t *hist, uint8_t *perm,
+                                        uint32_t lane)
+{
+    hist[lane] = 0u;
+    uint32_t st[5];
+#pragma unroll
+    for (int q = 0; q < 4; q++) st[q] = gs_lo(slot, 4u * lane + (uint32_t)q);
+    st[4] = gs_lo(slot, 4u * lane + 4u); /* [256] is the end bound for lane 63 */
+    const uint32_t endb = reinterpret_cast<const uint32_t *>(slot)[2u * kTile];
+    __builtin_amdgcn_wave_barrier();
+    uint32_t cls[4], rk[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t i = 4u * lane + (uint32_t)q;
+        const uint32_t e = i + 1u < cnt ? st[q + 1] : endb;
+        const uint32_t len = e - st[q];
+        cls[q] = i < cnt ? (len < 62u ? len : 62u) : 63u;
+        rk[q] = __hip_atomic_fetch_add(hist + cls[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t c = hist[lane];
+    uint32_t incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += v;
+    }
+    hist[lane] = incl - c;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < 4; q++) perm[hist[cls[q]] + rk[q]] = (uint8_t)(4u * lane + (uint32_t)q);
+}
+
+template <int MODE, int VAR>
+__global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__restrict__ keys_base,
+                                                            const uint64_t *__restrict__ off, uint64_t delta,
+                                                            uint64_t nkeys, uint32_t *__restrict__ out,
+                                                            uint64_t ntiles, WrDist dist)
+{
+    constexpr int kAux = 2; /* nt: read-once streams */
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kGsBytes];
+    uint8_t *perm2 = smem + kGsPerm;
+    uint32_t *hist = reinterpret_cast<uint32_t *>(smem + kGsHist);
+    uint32_t *tab = reinterpret_cast<uint32_t *>(smem + kGsTab);
+
+    const uint32_t t = threadIdx.x;
+    const uint32_t lane = t & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(t >> 6);
+    const uint64_t stride = gridDim.x;
+    uint64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    auto tile_at = [&](uint64_t j) -> uint64_t { /* j-th tile from here, clamped */
+        const uint64_t x = tile + j * stride;
+        return x < ntiles ? x : tile;
+    };
+    auto offs_slot = [&](uint32_t it) __attribute__((always_inline)) { return smem + kGsOffs + (it % 3u) * kGsOffSlot; };
+    auto slab_buf = [&](uint32_t it) __attribute__((always_inline)) { return smem + (it & 1u) * kGsCap; };
+    /* the slab of the tile whose offsets are in `slot`: its 16-aligned start and span */
+    auto bounds = [&](const uint8_t *slot, uint64_t &S16, uint64_t &span) __attribute__((always_inline)) {
+        const uint64_t *b = reinterpret_cast<const uint64_t *>(slot);
+        const uint64_t S = b[0] + delta, E = b[kTile] + delta;
+        S16 = S & ~(uint64_t)15;
+        span = E - S16;
+    };
+
+    if constexpr (uses_crc_table<MODE>()) tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
+    if constexpr (wg_dist<VAR>() == kDistKetama) tab[t] = cont_lower_bound(dist.cont, dist.ncont, t << 24);
+
+    /* prologue: offsets of tiles 0 and 1; then slab(0) and perm(0) */
+    gs_issue_offs<kAux>(off, tile_at(0), nkeys, offs_slot(0), t);
+    gs_issue_offs<kAux>(off, tile_at(1), nkeys, offs_slot(1), t);
+    full_barrier();
+    uint32_t cnt = tile_count(tile, nkeys);
+    uint64_t S16, span;
+    bounds(offs_slot(0), S16, span);
+    if (gs_fits(span)) issue_slab<kAux>(keys_base, S16, span, slab_buf(0), t);
+    if (wave == 0u) gs_sort(offs_slot(0), cnt, hist, perm2, lane);
+
+    uint64_t pend_idx = ~0ull;
+    uint32_t pend_h = 0;
+    for (uint32_t it = 0;; it++) {
+        full_barrier(); /* slab(it), offsets(it+1), perm(it) in LDS; every read of the buffers reused below done */
+        if (pend_idx != ~0ull) __builtin_nontemporal_store(pend_h, out + pend_idx);
+        pend_idx = ~0ull;
+        asm volatile("" ::: "memory");
+        const uint64_t t1 = tile + stride;
+        const bool more = t1 < ntiles;
+        const uint32_t cnt1 = more ? tile_count(t1, nkeys) : 0u;
+        /* wave 0 sorts tile t+1 before any DMA of this iteration is in
+         * flight: hipcc waits vmcnt(0) before an LDS atomic while an LDS-DMA
+         * may alias it */
+        if (more && wave == 0u) gs_sort(offs_slot(it + 1u), cnt1, hist, perm2 + ((it + 1u) & 1u) * kTile, lane);
+        asm volatile("" ::: "memory");
+        gs_issue_offs<kAux>(off, tile_at(2), nkeys, offs_slot(it + 2u), t);
+        uint64_t S16n = 0, spann = 0;
+        if (more) {
+            bounds(offs_slot(it + 1u), S16n, spann);
+            if (gs_fits(spann)) issue_slab<kAux>(keys_base, S16n, spann, slab_buf(it + 1u), t);
+        }
+        asm volatile("" ::: "memory");
+
+        /* this wave's length quartile of tile `tile` */
+        const uint8_t *slot = offs_slot(it);
+        const uint32_t j = 64u * wave + lane;
+        if (j < cnt) {
+            const uint32_t i = perm2[(it & 1u) * kTile + j];
+            const uint32_t s = gs_lo(slot, i);
+            const uint32_t e = i + 1u < cnt ? gs_lo(slot, i + 1u) : gs_lo(slot, kTile);
+            const uint32_t len = e - s;
+            const uint32_t pos = s + (uint32_t)delta - (uint32_t)S16;
+            uint32_t h;
+            if constexpr ((VAR & 8) != 0) {
+                h = pos ^ len; /* DIAGNOSTIC ONLY: the memory pipeline without hashing */
+            } else if (gs_fits(span)) {
+                LdsSrc src{reinterpret_cast<const uint32_t *>(slab_buf(it))};
+                h = wg_value<MODE, VAR>(src, pos, len, tab, tab, dist);
+            } else {
+                GlobalSrc src{reinterpret_cast<const uint32_t *>(keys_base)};
+                h = wg_value<MODE, VAR>(src, S16 + pos, len, tab, tab, dist);
+                __builtin_amdgcn_s_waitcnt(0x0070); /* retire the reader's loads before the paths merge */
+            }
+            pend_idx = tile * (uint64_t)kTile + i;
+            pend_h = h;
+        }
+        if (!more) break;
+        tile = t1;
+        cnt = cnt1;
+        S16 = S16n;
+        span = spann;
+    }
+    if (pend_idx != ~0ull) out[pend_idx] = pend_h;
+}
+
 /* ---------------- register-staged pipeline (variant bit 5) ----------------
  *
  * Same tiles, same hashing, different staging: every lane keeps the NEXT-BUT-
@@ -1561,8 +1756,13 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
                 uint32_t c = 64u * (uint32_t)i + lane;
                 if (c >= nch) c = nch - 1u; /* stay inside the key buffer (+ NC_GPUHASH_PAD) */
                 glds16<kNT>(keys_base + S16 + 16u * c, dst + 1024u * (uint32_t)i);
+            } else if (tile < ntiles) {
+                dummy(keys_base + S16); /* the tile's first 16-byte block: readable */
             } else {
-                dummy(keys_base + S16);
+                /* past the last tile S16 is 0, and keys_base itself need not be
+                 * readable (a batch's offsets may start anywhere: a chunk of a
+                 * larger CSR hands in keys - offsets[0]) */
+                dummy(off + nkeys);
             }
         }
     };
@@ -1790,6 +1990,7 @@ constexpr int kVarDirectIl32 = (8 | 2) << 20; /* a wave's tiles interleaved over
                                                  wave_tiles) */
 constexpr int kVarWsort = 1 << 24; /* the wave-sorted pipeline (nc_wsort_kernels.hip); options in bits 20-23 */
 constexpr int kVarNoFixedLen = 1 << 26; /* md5: no fixed-length specialisation (A/B) */
+constexpr int kVarGsort = 1 << 25; /* the grouped workgroup pipeline (nc_hash_kernel_gs); options in bits 20-23 */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -1911,6 +2112,43 @@ hipError_t launch_mode(const uint8_t *base, const uint64_t *off, uint64_t delta,
 {
     return sort ? launch_sorted<MODE, true>(base, off, delta, nkeys, out, stream, var)
                 : launch_sorted<MODE, false>(base, off, delta, nkeys, out, stream, var);
+}
+
+/* One grouped-workgroup launch (variant bit 25): a persistent grid of
+ * `sets` resident sets of workgroups (bits 21-22: 6, 1, 3, 8), so
+ * workgroups whose tiles ran short hand their slots to new ones. */
+template <int MODE, int VAR>
+hipError_t launch_gs(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                     hipStream_t stream, int var, const WrDist &dist = WrDist{nullptr, 0u, 0u})
+{
+    void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist) =
+        nc_hash_kernel_gs<MODE, VAR>;
+    static int per_cu = 0;
+    if (per_cu == 0) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, kBlock, 0) != hipSuccess || b <= 0) b = 4;
+        per_cu = b;
+    }
+    static const uint64_t kSets[4] = {6, 1, 3, 8};
+    const uint64_t ntiles = (nkeys + kTile - 1) / kTile;
+    const int cap = grid_cap();
+    uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu * kSets[(var >> 21) & 3];
+    if (grid > ntiles) grid = ntiles;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, stream, base, off, delta, nkeys, out, ntiles,
+                       dist);
+    return hipGetLastError();
+}
+
+/* bit 20: DIAGNOSTIC no-hash build (fnv1a_64 only; outputs are not hashes) */
+template <int MODE>
+hipError_t launch_gs_mode(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
+                          hipStream_t stream, int var)
+{
+    if constexpr (MODE == NC_GPUHASH_FNV1A_64) {
+        if (var & (1 << 20)) return launch_gs<MODE, 8>(base, off, delta, nkeys, out, stream, var);
+    }
+    return launch_gs<MODE, 0>(base, off, delta, nkeys, out, stream, var);
 }
 
 /* One wave-ring launch: a persistent grid of every resident workgroup slot
@@ -2045,6 +2283,7 @@ template <int MODE>
 hipError_t nc_tu::entry(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                         hipStream_t stream, bool sort, int var)
 {
+    if ((var & kVarGsort) != 0) return launch_gs_mode<MODE>(base, off, delta, nkeys, out, stream, var);
     if ((var & 128) != 0) return launch_wr_mode<MODE>(base, off, delta, nkeys, out, stream, var);
     return launch_mode<MODE>(base, off, delta, nkeys, out, stream, sort, var);
 }
@@ -2164,12 +2403,16 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
     /* varying lengths: a wave runs as long as its longest key; length-grouped
      * tiles and oversubscribed grids rebalance that */
     if (mean < 22u) { /* C2 */
-        /* one_at_a_time (the most VALU per byte): the wave-sorted pipeline,
-         * whose 6 KiB slab holds a 256-key tile of keys up to ~20 B on average
-         * (C2 0.585 -> 0.505 ms; fnv1a_64 stays 4 % faster on the workgroup
-         * x3, profiles/r02_wsort.jsonl) */
-        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return mean < 20u ? kVarWsort : kVarWorkgroup | kVarSorted | kVarOver;
-        return kVarWorkgroup | kVarOver;
+        /* the grouped workgroup pipeline (each wave hashes one length
+         * quartile of the tile; its 6 KiB slab holds a 256-key tile up to
+         * ~23 B per key): C2 fnv x4 0.449-0.454 -> 0.429-0.431 ms, hsieh 0.447
+         * -> 0.433, murmur 0.435 -> 0.425, jenkins 0.526 -> 0.445, crc16 0.690
+         * -> 0.645, one_at_a_time 0.504 (wave-sorted) -> 0.473 at three
+         * resident sets (profiles/r03_c2_gsort.jsonl); crc32 / crc32a tie
+         * the workgroup x6 and keep it */
+        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarGsort | (2 << 21);
+        if (mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A) return kVarWorkgroup | kVarOver;
+        return kVarGsort;
     }
     if (crc || mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarRegStaged | kVarOver;
     return kVarRegStaged;
@@ -2196,6 +2439,27 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
     }
     if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))
         return nc_wsort::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
+    if ((var & kVarGsort) != 0) {
+        switch (mode) {
+#define NC_CASE(M) \
+    case M: return nc_tu::entry<M>(base, d_off, delta, nkeys, d_out, stream, false, var);
+            NC_CASE(NC_GPUHASH_ONE_AT_A_TIME)
+            NC_CASE(NC_GPUHASH_MD5)
+            NC_CASE(NC_GPUHASH_CRC16)
+            NC_CASE(NC_GPUHASH_CRC32)
+            NC_CASE(NC_GPUHASH_CRC32A)
+            NC_CASE(NC_GPUHASH_FNV1_64)
+            NC_CASE(NC_GPUHASH_FNV1A_64)
+            NC_CASE(NC_GPUHASH_FNV1_32)
+            NC_CASE(NC_GPUHASH_FNV1A_32)
+            NC_CASE(NC_GPUHASH_HSIEH)
+            NC_CASE(NC_GPUHASH_MURMUR)
+            NC_CASE(NC_GPUHASH_JENKINS)
+#undef NC_CASE
+        default:
+            return hipErrorInvalidValue;
+        }
+    }
     var &= ~(kVarDirect | kVarWsort | kVarNoFixedLen | (15 << 20));
     const bool sort = sort_enabled() || (var & kVarSorted) != 0;
     var &= ~(kVarWorkgroup | kVarSorted); /* kVarOver rides along to launch_kernel */
@@ -2229,6 +2493,13 @@ rstatus_t fail(int err)
     return NC_ERROR;
 }
 
+/* a launch error, named on stderr when NC_GPUHASH_DEBUG is set */
+rstatus_t fail_launch(hipError_t e, const char *what)
+{
+    if (getenv("NC_GPUHASH_DEBUG") != nullptr) fprintf(stderr, "nc_gpuhash: %s: %s\n", what, hipGetErrorString(e));
+    return fail(e == hipErrorNoDevice ? ENODEV : EIO);
+}
+
 } // namespace
 
 extern "C" rstatus_t nc_gpuhash_batch_device_shaped(int mode, const uint8_t *d_keys, const uint64_t *d_offsets,
@@ -2239,7 +2510,7 @@ extern "C" rstatus_t nc_gpuhash_batch_device_shaped(int mode, const uint8_t *d_k
     if (nkeys == 0) return NC_OK;
     if (d_keys == nullptr || d_offsets == nullptr || d_out == nullptr) return fail(EINVAL);
     hipError_t err = launch(mode, d_keys, d_offsets, nkeys, d_out, reinterpret_cast<hipStream_t>(stream), shape);
-    if (err != hipSuccess) return fail(err == hipErrorNoDevice ? ENODEV : EIO);
+    if (err != hipSuccess) return fail_launch(err, "nc_gpuhash_batch_device_shaped");
     return NC_OK;
 }
 

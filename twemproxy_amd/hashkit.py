@@ -513,6 +513,52 @@ class Context:
         self._keep.pop(ticket, None)
 
 
+class Pipe:
+    """nc_gpuhash_pipe: whole host batches from caller-pinned memory, chunked
+    H2D / kernel / D2H on three streams, no repacking (the large-batch host
+    path, SURVEY.md §8d end to end)."""
+
+    def __init__(self, device: int = 0, chunk_keys: int = 1 << 22, chunk_bytes: int = 1 << 26, depth: int = 3):
+        self._lib = L.lib()
+        self._h = self._lib.nc_gpuhash_pipe_create(device, chunk_keys, chunk_bytes, depth)
+        if not self._h:
+            raise L.NcError(ctypes.get_errno(), "nc_gpuhash_pipe_create failed")
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.nc_gpuhash_pipe_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def hash(self, hash_: int | str, keys, offsets, out, nkeys: int | None = None, shape=None) -> None:
+        """keys / offsets / out: pinned host tensors (torch pin_memory) or
+        addresses of pinned memory; uint8 keys readable NC_GPUHASH_PAD bytes
+        past offsets[nkeys], int64/uint64 offsets, int32/uint32 out. Blocks
+        until every hash is in `out`."""
+        def addr(x):
+            return x if isinstance(x, int) else x.data_ptr()
+
+        if nkeys is None:
+            nkeys = offsets.numel() - 1
+        L.check(self._lib.nc_gpuhash_batch_pinned(self._h, mode_of(hash_), addr(keys), addr(offsets), nkeys,
+                                                   addr(out), _shape_arg(shape), 0),
+                "nc_gpuhash_batch_pinned")
+
+
+def host_register(ptr: int, nbytes: int) -> None:
+    """Page-lock and map an existing host range (nc_gpuhash_host_register)."""
+    L.check(L.lib().nc_gpuhash_host_register(ptr, nbytes), "nc_gpuhash_host_register")
+
+
+def host_unregister(ptr: int) -> None:
+    L.check(L.lib().nc_gpuhash_host_unregister(ptr), "nc_gpuhash_host_unregister")
+
+
 # ---------------------------------------------------------------- synthetic keys
 
 SYNTH_FIXED, SYNTH_ZIPF, SYNTH_UNIFORM = 0, 1, 2

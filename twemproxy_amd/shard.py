@@ -16,6 +16,11 @@ import torch.distributed as dist
 
 from ._lib import NC_GPUHASH_PAD
 
+# Largest single point-to-point message of the scatter: a C4 shard is 8 GiB;
+# it goes as 1 GiB pieces (all inside one group), so no count or size inside
+# the transport ever approaches 2^31 elements.
+MAX_MSG_BYTES = 1 << 30
+
 
 def plan_bounds(offsets: torch.Tensor, nshards: int) -> torch.Tensor:
     """Key bounds (nshards + 1, int64) splitting offsets' bytes evenly.
@@ -39,6 +44,21 @@ def plan_bounds(offsets: torch.Tensor, nshards: int) -> torch.Tensor:
     zero = torch.zeros(1, dtype=torch.int64, device=offsets.device)
     end = torch.full((1,), n, dtype=torch.int64, device=offsets.device)
     return torch.cat([zero, cuts.to(torch.int64), end])
+
+
+def _pieces(t: torch.Tensor, max_bytes: int | None = None):
+    """A 1-D tensor as contiguous views of at most max_bytes (MAX_MSG_BYTES)
+    each; both ends cut it the same way, so sends and receives pair up in
+    order."""
+    step = max(1, (max_bytes or MAX_MSG_BYTES) // max(1, t.element_size()))
+    return [t[i: i + step] for i in range(0, t.numel(), step)]
+
+
+def shard_of(keys: torch.Tensor, offsets: torch.Tensor, kb, bb, r: int):
+    """Rank r's shard as the root holds it: views of the key bytes
+    [bb[r], bb[r+1]) and offsets [kb[r], kb[r+1]] of the full batch (not yet
+    rebased). Used for the root's own shard and for the sends."""
+    return keys[bb[r]: bb[r + 1]], offsets[kb[r]: kb[r + 1] + 1]
 
 
 def scatter_shards(keys: torch.Tensor | None, offsets: torch.Tensor | None, device: torch.device,
@@ -66,18 +86,16 @@ def scatter_shards(keys: torch.Tensor | None, offsets: torch.Tensor | None, devi
     ops = []
     if rank == root:
         for r in range(world):
-            rk0, rk1, rb0, rb1 = kb[r], kb[r + 1], bb[r], bb[r + 1]
+            ks, os_ = shard_of(keys, offsets, kb, bb, r)
             if r == root:
-                local_keys[: bhi - blo].copy_(keys[blo:bhi])
-                local_off.copy_(offsets[klo: khi + 1])
+                local_keys[: bhi - blo].copy_(ks)
+                local_off.copy_(os_)
                 continue
-            ops.append(dist.P2POp(dist.isend, offsets[rk0: rk1 + 1].contiguous(), r, group))
-            if rb1 > rb0:
-                ops.append(dist.P2POp(dist.isend, keys[rb0:rb1].contiguous(), r, group))
+            for piece in _pieces(os_) + _pieces(ks):
+                ops.append(dist.P2POp(dist.isend, piece, r, group))
     else:
-        ops.append(dist.P2POp(dist.irecv, local_off, root, group))
-        if bhi > blo:
-            ops.append(dist.P2POp(dist.irecv, local_keys[: bhi - blo], root, group))
+        for piece in _pieces(local_off) + _pieces(local_keys[: bhi - blo]):
+            ops.append(dist.P2POp(dist.irecv, piece, root, group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
