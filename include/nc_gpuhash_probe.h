@@ -67,7 +67,8 @@ rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const u
  * tiles per wave, bit 22 DIAGNOSTIC no-hash build (fnv1a_64), bit 23 its
  * tiles interleaved over the grid; bit 25: the grouped workgroup pipeline
  * (each wave one length quartile of the tile), bit 20 its DIAGNOSTIC no-hash
- * build (fnv1a_64), bits 21-22 its resident sets (6, 1, 3, 8); bit 26: md5
+ * build (fnv1a_64), bits 21-22 its resident sets (6, 1, 3, 8), bit 23 three
+ * slab buffers, bit 27 one coalesced store per tile; bit 26: md5
  * without its fixed-length specialisation (A/B); -1 = keep). */
 rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 

@@ -44,7 +44,9 @@ def gpu_hash(mode, keys_d, off_d):
                         (0, 0, 65536 | (1 << 18)), (0, 1, 32 | (1 << 18)), (0, 0, 1 << 19),
                         (0, 0, (1 << 19) | (4 << 20)), (0, 0, (1 << 19) | (10 << 20)),
                         (0, 0, (1 << 19) | (14 << 20)), (0, 0, 1 << 24), (0, 0, (1 << 24) | (9 << 20)),
-                        (0, 0, 1 << 25), (37, 0, 1 << 25), (0, 0, (1 << 25) | (1 << 21))],
+                        (0, 0, 1 << 25), (37, 0, 1 << 25), (0, 0, (1 << 25) | (1 << 21)),
+                        (0, 0, (1 << 25) | (1 << 23)), (11, 0, (1 << 25) | (1 << 23) | (2 << 21)),
+                        (0, 0, (1 << 25) | (1 << 27))],
                 ids=["persistent+sort", "auto", "workgroup", "grid37+sort+shiftadd", "shiftadd", "grid5+sort",
                      "sorted_bit", "regstage", "regstage+sort", "grid11+regstage+sort+shiftadd", "grid9+regstage",
                      "cached", "cached+sort", "regstage+cached", "grid7+regstage+cached+sort", "wavering",
@@ -53,7 +55,7 @@ def gpu_hash(mode, keys_d, off_d):
                      "wavering_t64_w4", "wavering_t256_sorted", "grid7+wavering_t256_sorted_w4_6_2_3",
                      "wavering_t256_sorted_5_1_2", "workgroup_over3", "regstage+sort+over3", "direct",
                      "direct_lines", "direct_il32", "direct_lines_il32", "wsort", "wsort_il4",
-                     "gsort", "grid37+gsort", "gsort_1set"])
+                     "gsort", "grid37+gsort", "gsort_1set", "gsort_d3", "grid11+gsort_d3_3sets", "gsort_cs"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)
@@ -240,7 +242,10 @@ def test_sort_and_grid_variants_agree_full_size(gpu):
                             (1536, 0, 32), (2048, 1, 32), (0, 0, 64), (0, 1, 64), (0, 0, 96), (1536, 1, 96),
                             (0, 0, 128), (1, 0, 128), (7, 0, 384), (0, 0, 640), (2048, 0, 896), (0, 0, 129),
                             (0, 0, 192), (0, 0, 1 << 24), (0, 0, (1 << 24) | (2 << 20)), (0, 0, (1 << 24) | (8 << 20)),
-                            (0, 0, 1 << 25), (1, 0, 1 << 25), (4096, 0, 1 << 25), (0, 0, (1 << 25) | (3 << 21))):
+                            (0, 0, 1 << 25), (1, 0, 1 << 25), (4096, 0, 1 << 25), (0, 0, (1 << 25) | (3 << 21)),
+                            (0, 0, (1 << 25) | (1 << 23)), (1, 0, (1 << 25) | (1 << 23)),
+                            (777, 0, (1 << 25) | (1 << 23)), (0, 0, (1 << 25) | (1 << 27)),
+                            (0, 0, (1 << 25) | (1 << 23) | (1 << 27))):
         L.lib().nc_gpuhash_set_tuning(grid, sort, var)
         out = t.hash_batch_device("fnv1a_64", kd, od)
         torch.cuda.synchronize()
@@ -458,8 +463,11 @@ def test_wsort_round_of_long_keys(gpu, oracle, var):
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
 
 
-@pytest.mark.parametrize("tune", [(0, 1 << 25), (0, (1 << 25) | (1 << 21)), (3, 1 << 25), (1, (1 << 25) | (3 << 21))],
-                         ids=["gsort6", "gsort1", "grid3", "grid1_8sets"])
+@pytest.mark.parametrize("tune", [(0, 1 << 25), (0, (1 << 25) | (1 << 21)), (3, 1 << 25), (1, (1 << 25) | (3 << 21)),
+                                  (0, (1 << 25) | (1 << 23)), (2, (1 << 25) | (1 << 23)),
+                                  (0, (1 << 25) | (1 << 23) | (1 << 21)), (0, (1 << 25) | (1 << 27)),
+                                  (5, (1 << 25) | (1 << 23) | (1 << 27))],
+                         ids=["gsort6", "gsort1", "grid3", "grid1_8sets", "d3", "d3_grid2", "d3_1set", "cs", "d3_cs_grid5"])
 def test_gsort_ragged_tiles(gpu, oracle, tune):
     """The grouped workgroup pipeline (variant bit 25: offsets by LDS-DMA two
     tiles ahead, wave 0 sorting the next tile, each wave one length quartile)
@@ -485,6 +493,13 @@ def test_gsort_ragged_tiles(gpu, oracle, tune):
                 kd2, od2 = kd, od[1:].contiguous()
                 np.testing.assert_array_equal(gpu_hash(6, kd2, od2), oracle.batch(6, keys, off)[1:],
                                               err_msg=f"tune={tune} n={n} offset base")
+                import torch  # an output buffer that is only 4-byte aligned
+
+                ob = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+                t.hash_batch_device(6, kd, od, out=ob[1:])
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(ob[1:].cpu().numpy().view(np.uint32), oracle.batch(6, keys, off),
+                                              err_msg=f"tune={tune} n={n} misaligned out")
     finally:
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
 
@@ -508,7 +523,7 @@ def test_virtual_key_base(gpu, oracle):
         out = torch.empty(n, dtype=torch.int32, device="cuda")
         shape = L.NcShape(int(off[-1]), *spec.len_range())
         for var in (0, 65536, 32, 128, 896, 1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (14 << 20), 1 << 24,
-                    1 << 25):
+                    1 << 25, (1 << 25) | (1 << 23), (1 << 25) | (1 << 27)):
             L.lib().nc_gpuhash_set_tuning(0, 0, var)
             try:
                 for m in MODES:

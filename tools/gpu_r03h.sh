@@ -1,0 +1,6 @@
+set -u
+O=gpurun_out/r03h
+mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -k "gsort or full_size or beyond_4gib or virtual" > $O/pytest_gsort.log 2>&1 || exit $?
+timeout -k 10 400 python3 tools/ab.py --configs C2 --modes fnv1a_64,one_at_a_time,jenkins,crc32 --variants 0,35651584,41943040,44040192,46137344,42991616,34603008 --rounds 3 --iters 10 > $O/ab_c2.jsonl 2> $O/ab_c2.err || exit $?
+echo done

@@ -1029,111 +1029,156 @@ __global__ __launch_bounds__(kBlock, kMinWaves<MODE>()) void nc_hash_kernel(cons
     if (pend_idx != ~0ull) out[pend_idx] = pend_h;
 }
 
+typedef __attribute__((address_space(3))) const void lds_cvoid_t;
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p)
+{
+    return (uint32_t)(uintptr_t)(lds_cvoid_t *)p;
+}
+
 /* ---------------- grouped workgroup pipeline (variant bit 25) ----------------
  *
- * The workgroup pipeline's tiles (256 keys, 4 waves, LDS-DMA slab double
- * buffer, one barrier per tile), with each WAVE hashing one length quartile
- * of the tile instead of 64 neighbouring keys: a wave runs as long as its
- * longest key, so under Zipf 8-64 B four unsorted waves cost ~4 x 61 byte
- * steps per tile, four length-grouped ones ~110. The grouping costs no
- * barrier: a tile's offsets arrive by LDS-DMA two tiles ahead (the whole
- * workgroup sees them after the top barrier), and wave 0 — which hashes the
- * shortest quartile — counting-sorts tile t+1 while the others hash tile t,
- * leaving the permutation in LDS for the next iteration. Offsets are read
- * from HBM once, as 16-byte pieces (the plain pipeline reads each twice,
- * 4 bytes per lane).
+ * The workgroup pipeline's tiles (256 keys, 4 waves, LDS-DMA slabs, one
+ * barrier per tile), with each WAVE hashing one length quartile of the tile
+ * instead of 64 neighbouring keys: a wave runs as long as its longest key,
+ * so under Zipf 8-64 B four unsorted waves cost ~4 x 61 byte steps per tile,
+ * four length-grouped ones ~110. The grouping costs no barrier: a tile's
+ * offsets arrive by LDS-DMA D tiles ahead (the whole workgroup sees them
+ * after a top barrier), and wave 0 — which hashes the shortest quartile —
+ * counting-sorts tile t+1 while the others hash tile t, leaving the
+ * permutation in LDS for the next iteration. Offsets are read from HBM once,
+ * the low dword of each (lengths and slab positions are 32-bit; the tile
+ * bounds' high dwords come separately).
  *
- * Iteration t (after the top barrier: slab(t), offsets(t+1) and perm(t) are
- * in LDS): pending stores of tile t-1; DMA offsets(t+2) and slab(t+1); wave 0
- * sorts tile t+1; every wave hashes its quartile of tile t. */
-constexpr uint32_t kGsOffSlot = 2064;                  /* off[k0 .. k0+255] + end bound at [256], 16-aligned */
-constexpr uint32_t kGsCap = 6144;                      /* per slab buffer: Zipf 8-64 B tiles need ~5 KiB */
-constexpr uint32_t kGsOffs = 2 * kGsCap;               /* u64[3][258] */
-constexpr uint32_t kGsPerm = kGsOffs + 3 * kGsOffSlot; /* u8[2][256]: sorted position -> key index */
-constexpr uint32_t kGsHist = kGsPerm + 2 * kTile;      /* u32[64], the sorter's counters */
-constexpr uint32_t kGsTab = kGsHist + 4 * 64;          /* u32[256]: crc table / ketama bucket index */
-constexpr uint32_t kGsBytes = kGsTab + 4 * 256;
-static_assert(kGsBytes <= kLdsBudget, "8 workgroups per CU");
-static_assert(kGsOffs % 16 == 0 && kGsOffSlot % 16 == 0 && kGsTab % 16 == 0, "LDS carve must stay 16-byte aligned");
+ * D = 2: slab(t+1) in flight while tile t hashes (8 workgroups per CU, the
+ * top barrier waits for everything). D = 3: slabs t+1 and t+2 in flight (7
+ * workgroups per CU): every wave issues exactly kSlabIters slab DMAs per
+ * tile (dummies where a slab needs fewer), so the top barrier waits with a
+ * counted vmcnt that leaves the youngest slab in flight; the sorter's LDS
+ * writes are inline asm, which hipcc does not hold behind that DMA.
+ *
+ * Iteration t (after the top barrier: slab(t), offsets(t+1 .. t+D-1) and
+ * perm(t) in LDS): pending stores of tile t-1; wave 0 sorts tile t+1; DMA
+ * offsets(t+D) and slab(t+D-1); every wave hashes its quartile of tile t. */
+template <int D, bool CS>
+struct GsLds {
+    static_assert(D == 2 || D == 3, "two or three slab buffers");
+    static constexpr uint32_t kOffSlot = 1040; /* u32 lo[256], then end lo / hi and start hi */
+    static constexpr uint32_t kNOff = D + 1;    /* offsets of tiles t .. t+D */
+    static constexpr uint32_t kResBytes = CS ? 2u * 4u * kTile : 0u; /* u32[2][256]: hashes by key, for one coalesced store */
+    static constexpr uint32_t kFixed = kNOff * kOffSlot + 2 * kTile + 4 * 64 + 4 * 256 + 16 + kResBytes;
+    static constexpr uint32_t kBudget = D == 2 ? 20480 : 23392; /* 8 / 7 workgroups per CU */
+    static constexpr uint32_t kCap = ((kBudget - kFixed) / D) & ~15u;
+    static constexpr uint32_t kOffs = D * kCap;
+    static constexpr uint32_t kPerm = kOffs + kNOff * kOffSlot; /* u8[2][256]: sorted position -> key index */
+    static constexpr uint32_t kHist = kPerm + 2 * kTile;        /* u32[64], the sorter's counters */
+    static constexpr uint32_t kTab = kHist + 4 * 64;            /* u32[256]: crc table / ketama bucket index */
+    static constexpr uint32_t kDump = kTab + 4 * 256;           /* landing area of dummy DMAs */
+    static constexpr uint32_t kRes = kDump + 16;
+    static constexpr uint32_t kBytes = kRes + kResBytes;
+    static constexpr int kSlabIters = (int)((kCap / 16 + kBlock - 1) / kBlock);
+    static_assert(kBytes <= kBudget, "LDS budget");
+    static_assert(kOffs % 16 == 0 && kTab % 16 == 0 && kCap % 16 == 0, "LDS carve must stay 16-byte aligned");
+};
 
-__device__ __forceinline__ bool gs_fits(uint64_t span) { return span + 48u <= (uint64_t)kGsCap; }
-
-/* offsets of `tile` into slot: off[k0 .. k0+255] as 128 16-byte pieces (waves
- * 0-1, pairs clamped inside off[0 .. nkeys]) and the end bound off[k0+cnt]
- * at [256] (wave 2, two dwords) */
+/* low dwords of off[k0 .. k0+255] (clamped at nkeys) into slot, one 4-byte
+ * DMA per lane; wave 0 adds the end bound off[k0+cnt] (low, high) and the
+ * start's high dword at [256..258] */
 template <int AUX>
 __device__ __forceinline__ void gs_issue_offs(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
                                               uint8_t *slot, uint32_t t)
 {
     const uint64_t k0 = tile * (uint64_t)kTile;
-    if (t < 128u) {
-        const uint64_t last_pair = (nkeys - 1u) & ~(uint64_t)1; /* off[p], off[p+1] stay <= nkeys */
-        uint64_t p = k0 + 2u * t;
-        if (p > last_pair) p = last_pair;
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)(off + p), (lds_void_t *)(slot + 16u * (t & ~63u)), 16, 0,
-                                         AUX);
-    } else if (t < 130u) {
+    uint64_t k = k0 + t;
+    if (k > nkeys) k = nkeys;
+    const uint32_t *o32 = reinterpret_cast<const uint32_t *>(off);
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)(o32 + 2u * k), (lds_void_t *)(slot + 4u * (t & ~63u)), 4, 0, AUX);
+    if (t < 3u) {
         const uint64_t e = k0 + tile_count(tile, nkeys);
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)(reinterpret_cast<const uint32_t *>(off + e) + (t - 128u)),
-                                         (lds_void_t *)(slot + 8u * kTile), 4, 0, AUX);
+        const uint32_t *src = t == 0u ? o32 + 2u * e : t == 1u ? o32 + 2u * e + 1u : o32 + 2u * k0 + 1u;
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)src, (lds_void_t *)(slot + 4u * kTile), 4, 0, AUX);
     }
 }
 
-/* low dword of the start of key i (< cnt) and of its end, from an offsets slot */
+typedef unsigned int gs_u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ uint32_t gs_lo(const uint8_t *slot, uint32_t i)
 {
-    return reinterpret_cast<const uint32_t *>(slot)[2u * i];
+    return reinterpret_cast<const uint32_t *>(slot)[i];
+}
+
+/* LDS ops of the sorter as inline asm: hipcc would wait vmcnt(0) before an
+ * LDS write while an LDS-DMA is in flight; a wave's LDS operations complete
+ * in order, and results are tied to an explicit lgkmcnt wait */
+__device__ __forceinline__ void gs_ds_write_b32(uint32_t a, uint32_t v)
+{
+    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void gs_ds_write_b8(uint32_t a, uint32_t v)
+{
+    asm volatile("ds_write_b8 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t gs_ds_add_rtn(uint32_t a, uint32_t v)
+{
+    uint32_t r;
+    asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(v) : "memory");
+    return r;
+}
+__device__ __forceinline__ uint32_t gs_ds_read_b32(uint32_t a)
+{
+    uint32_t r;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(a) : "memory");
+    return r;
 }
 
 /* counting sort of the tile in `slot` by length class (one wave): perm[pos]
- * = key index, ascending classes; absent keys (>= cnt) last (class 63; valid
- * keys clamp to 62) */
-__device__ __forceinline__ void gs_sort(const uint8_t *slot, uint32_t cnt, uint32_t *hist, uint8_t *perm,
-                                        uint32_t lane)
+ * = key index, ascending classes; absent keys (>= cnt) last (class 63;
+ * valid keys clamp to 62). hist / perm are LDS byte addresses. */
+__device__ __forceinline__ void gs_sort(const uint8_t *slot, uint32_t cnt, uint32_t hist, uint32_t perm, uint32_t lane)
 {
-    hist[lane] = 0u;
+    gs_ds_write_b32(hist + 4u * lane, 0u);
+    const uint32_t sa = lds_addr(slot) + 16u * lane;
     uint32_t st[5];
 #pragma unroll
-    for (int q = 0; q < 4; q++) st[q] = gs_lo(slot, 4u * lane + (uint32_t)q);
-    st[4] = gs_lo(slot, 4u * lane + 4u); /* [256] is the end bound for lane 63 */
-    const uint32_t endb = reinterpret_cast<const uint32_t *>(slot)[2u * kTile];
-    __builtin_amdgcn_wave_barrier();
+    for (int q = 0; q < 5; q++) st[q] = gs_ds_read_b32(sa + 4u * (uint32_t)q); /* [256] is lane 63's end bound */
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(st[0]), "+v"(st[1]), "+v"(st[2]), "+v"(st[3]), "+v"(st[4])::"memory");
     uint32_t cls[4], rk[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const uint32_t i = 4u * lane + (uint32_t)q;
-        const uint32_t e = i + 1u < cnt ? st[q + 1] : endb;
-        const uint32_t len = e - st[q];
+        const uint32_t len = st[q + 1] - st[q]; /* key 255 ends at the end bound, [256] */
         cls[q] = i < cnt ? (len < 62u ? len : 62u) : 63u;
-        rk[q] = __hip_atomic_fetch_add(hist + cls[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        rk[q] = gs_ds_add_rtn(hist + 4u * cls[q], 1u);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t c = hist[lane];
+    uint32_t c = gs_ds_read_b32(hist + 4u * lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rk[0]), "+v"(rk[1]), "+v"(rk[2]), "+v"(rk[3]), "+v"(c)::"memory");
     uint32_t incl = c;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t v = __shfl_up(incl, d, 64);
         if (lane >= (uint32_t)d) incl += v;
     }
-    hist[lane] = incl - c;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
+    gs_ds_write_b32(hist + 4u * lane, incl - c);
+    uint32_t b[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) perm[hist[cls[q]] + rk[q]] = (uint8_t)(4u * lane + (uint32_t)q);
+    for (int q = 0; q < 4; q++) b[q] = gs_ds_read_b32(hist + 4u * cls[q]);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
+#pragma unroll
+    for (int q = 0; q < 4; q++) gs_ds_write_b8(perm + b[q] + rk[q], 4u * lane + (uint32_t)q);
 }
 
-template <int MODE, int VAR>
+template <int MODE, int VAR, int D, bool CS>
 __global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__restrict__ keys_base,
                                                             const uint64_t *__restrict__ off, uint64_t delta,
                                                             uint64_t nkeys, uint32_t *__restrict__ out,
                                                             uint64_t ntiles, WrDist dist)
 {
+    using G = GsLds<D, CS>;
     constexpr int kAux = 2; /* nt: read-once streams */
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kGsBytes];
-    uint8_t *perm2 = smem + kGsPerm;
-    uint32_t *hist = reinterpret_cast<uint32_t *>(smem + kGsHist);
-    uint32_t *tab = reinterpret_cast<uint32_t *>(smem + kGsTab);
+    __shared__ __attribute__((aligned(16))) uint8_t smem[G::kBytes];
+    const uint8_t *perm2 = smem + G::kPerm;
+    uint32_t *tab = reinterpret_cast<uint32_t *>(smem + G::kTab);
+    const uint32_t lds_base = lds_addr(smem);
 
     const uint32_t t = threadIdx.x;
     const uint32_t lane = t & 63u;
@@ -1145,50 +1190,127 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__res
         const uint64_t x = tile + j * stride;
         return x < ntiles ? x : tile;
     };
-    auto offs_slot = [&](uint32_t it) __attribute__((always_inline)) { return smem + kGsOffs + (it % 3u) * kGsOffSlot; };
-    auto slab_buf = [&](uint32_t it) __attribute__((always_inline)) { return smem + (it & 1u) * kGsCap; };
+    auto offs_slot = [&](uint32_t it) __attribute__((always_inline)) {
+        return smem + G::kOffs + (it % G::kNOff) * G::kOffSlot;
+    };
+    auto slab_buf = [&](uint32_t it) __attribute__((always_inline)) { return smem + (it % (uint32_t)D) * G::kCap; };
     /* the slab of the tile whose offsets are in `slot`: its 16-aligned start and span */
+    /* (inline-asm reads: hipcc would hold a plain LDS read of a slot behind
+     * the slab DMA in flight, vmcnt(0), not knowing the two are disjoint) */
     auto bounds = [&](const uint8_t *slot, uint64_t &S16, uint64_t &span) __attribute__((always_inline)) {
-        const uint64_t *b = reinterpret_cast<const uint64_t *>(slot);
-        const uint64_t S = b[0] + delta, E = b[kTile] + delta;
+        const uint32_t a = lds_addr(slot);
+        uint32_t s_lo = gs_ds_read_b32(a), e_lo = gs_ds_read_b32(a + 4u * kTile);
+        uint32_t e_hi = gs_ds_read_b32(a + 4u * kTile + 4u), s_hi = gs_ds_read_b32(a + 4u * kTile + 8u);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(s_lo), "+v"(e_lo), "+v"(e_hi), "+v"(s_hi)::"memory");
+        const uint64_t S = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(s_hi) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane(s_lo)) + delta;
+        const uint64_t E = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(e_hi) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane(e_lo)) + delta;
         S16 = S & ~(uint64_t)15;
         span = E - S16;
+    };
+    auto fits = [&](uint64_t span) __attribute__((always_inline)) { return span + 48u <= (uint64_t)G::kCap; };
+    /* slab DMA of one tile: D = 2 as many instructions as its span needs;
+     * D = 3 exactly kSlabIters per wave (dummies past the span) */
+    auto slab_dma = [&](bool in, uint64_t S16, uint64_t span, uint8_t *buf) __attribute__((always_inline)) {
+        const uint32_t nch = in ? (uint32_t)((span + 15u) >> 4) + 2u : 0u; /* +2 pieces: reader look-ahead */
+        const uint32_t wbase = t & ~63u;
+#pragma unroll
+        for (int i = 0; i < G::kSlabIters; i++) {
+            const uint32_t c = t + (uint32_t)i * kBlock;
+            if (wbase + (uint32_t)i * kBlock < nch) {
+                if (c < nch)
+                    __builtin_amdgcn_global_load_lds((gbl_void_t *)(keys_base + S16 + 16u * c),
+                                                     (lds_void_t *)(buf + 16u * (wbase + (uint32_t)i * kBlock)), 16,
+                                                     0, kAux);
+            } else if (D == 3 && lane == 0u) {
+                __builtin_amdgcn_global_load_lds((gbl_void_t *)(off + nkeys), (lds_void_t *)(smem + G::kDump), 4, 0,
+                                                 0);
+            }
+        }
+    };
+    auto top_barrier = [&]() __attribute__((always_inline)) {
+        if constexpr (D == 2) {
+            full_barrier();
+        } else {
+            /* everything but the youngest slab's kSlabIters DMAs */
+            static_assert(G::kSlabIters <= 15, "vmcnt field");
+            __builtin_amdgcn_s_waitcnt(0x0070 | G::kSlabIters); /* vmcnt(kSlabIters) expcnt(7) lgkmcnt(0) */
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
     };
 
     if constexpr (uses_crc_table<MODE>()) tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
     if constexpr (wg_dist<VAR>() == kDistKetama) tab[t] = cont_lower_bound(dist.cont, dist.ncont, t << 24);
 
-    /* prologue: offsets of tiles 0 and 1; then slab(0) and perm(0) */
-    gs_issue_offs<kAux>(off, tile_at(0), nkeys, offs_slot(0), t);
-    gs_issue_offs<kAux>(off, tile_at(1), nkeys, offs_slot(1), t);
+    /* prologue: offsets of tiles 0 .. D-1; perm(0); slabs 0 .. D-2 */
+#pragma unroll
+    for (uint32_t j = 0; j < (uint32_t)D; j++) gs_issue_offs<kAux>(off, tile_at(j), nkeys, offs_slot(j), t);
     full_barrier();
     uint32_t cnt = tile_count(tile, nkeys);
+    if (wave == 0u) gs_sort(offs_slot(0), cnt, lds_base + G::kHist, lds_base + G::kPerm, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     uint64_t S16, span;
     bounds(offs_slot(0), S16, span);
-    if (gs_fits(span)) issue_slab<kAux>(keys_base, S16, span, slab_buf(0), t);
-    if (wave == 0u) gs_sort(offs_slot(0), cnt, hist, perm2, lane);
+    slab_dma(fits(span), S16, span, slab_buf(0));
+    if constexpr (D == 3) {
+        uint64_t s1, p1;
+        bounds(offs_slot(1), s1, p1);
+        slab_dma(tile_at(1) != tile && fits(p1), s1, p1, slab_buf(1));
+    }
 
     uint64_t pend_idx = ~0ull;
     uint32_t pend_h = 0;
+    /* CS: the previous tile's hashes, left in LDS by key index, go out as one
+     * 16-byte-per-lane store of wave 1 (a partial or misaligned tile: one
+     * dword per thread) */
+    uint64_t pend_tile = ~0ull;
+    uint32_t pend_cnt = 0, pend_par = 0;
+    const bool out16 = (reinterpret_cast<uintptr_t>(out) & 15u) == 0u;
+    auto store_tile = [&]() __attribute__((always_inline)) {
+        const uint32_t ra = lds_base + G::kRes + pend_par * 4u * kTile;
+        uint32_t *dst = out + pend_tile * (uint64_t)kTile;
+        if (pend_cnt == kTile && out16) {
+            if (wave == 1u) {
+                gs_u32x4 v;
+                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ra + 16u * lane) : "memory");
+                __builtin_nontemporal_store(v, reinterpret_cast<gs_u32x4 *>(dst) + lane);
+            }
+        } else if (t < pend_cnt) {
+            uint32_t v;
+            asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ra + 4u * t) : "memory");
+            __builtin_nontemporal_store(v, dst + t);
+        }
+    };
     for (uint32_t it = 0;; it++) {
-        full_barrier(); /* slab(it), offsets(it+1), perm(it) in LDS; every read of the buffers reused below done */
-        if (pend_idx != ~0ull) __builtin_nontemporal_store(pend_h, out + pend_idx);
-        pend_idx = ~0ull;
+        top_barrier(); /* slab(it), offsets(it+1 .. it+D-1), perm(it) in LDS; reads of reused buffers done */
+        if constexpr (CS) {
+            if (pend_tile != ~0ull) store_tile();
+        } else {
+            if (pend_idx != ~0ull) __builtin_nontemporal_store(pend_h, out + pend_idx);
+            pend_idx = ~0ull;
+        }
         asm volatile("" ::: "memory");
         const uint64_t t1 = tile + stride;
         const bool more = t1 < ntiles;
         const uint32_t cnt1 = more ? tile_count(t1, nkeys) : 0u;
-        /* wave 0 sorts tile t+1 before any DMA of this iteration is in
-         * flight: hipcc waits vmcnt(0) before an LDS atomic while an LDS-DMA
-         * may alias it */
-        if (more && wave == 0u) gs_sort(offs_slot(it + 1u), cnt1, hist, perm2 + ((it + 1u) & 1u) * kTile, lane);
+        /* every LDS read of the offsets slots comes before this iteration's
+         * DMAs: hipcc waits vmcnt(0) before an LDS read it cannot prove
+         * disjoint from an LDS-DMA in flight */
+        uint64_t S16n = 0, spann = 0, sn, pn;
+        if (more) bounds(offs_slot(it + 1u), S16n, spann);
+        bounds(offs_slot(it + (uint32_t)D - 1u), sn, pn); /* slab(t + D - 1) */
+        const bool dn = tile + (uint64_t)(D - 1) * stride < ntiles && fits(pn);
+        gs_issue_offs<kAux>(off, tile_at(D), nkeys, offs_slot(it + (uint32_t)D), t);
+        slab_dma(dn, sn, pn, slab_buf(it + (uint32_t)D - 1u));
         asm volatile("" ::: "memory");
-        gs_issue_offs<kAux>(off, tile_at(2), nkeys, offs_slot(it + 2u), t);
-        uint64_t S16n = 0, spann = 0;
-        if (more) {
-            bounds(offs_slot(it + 1u), S16n, spann);
-            if (gs_fits(spann)) issue_slab<kAux>(keys_base, S16n, spann, slab_buf(it + 1u), t);
-        }
+        /* wave 0 sorts tile t+1 with its DMAs already out (every LDS access
+         * of the sort is inline asm, which hipcc does not hold behind them) */
+        if (more && wave == 0u)
+            gs_sort(offs_slot(it + 1u), cnt1, lds_base + G::kHist, lds_base + G::kPerm + ((it + 1u) & 1u) * kTile,
+                    lane);
         asm volatile("" ::: "memory");
 
         /* this wave's length quartile of tile `tile` */
@@ -1197,13 +1319,14 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__res
         if (j < cnt) {
             const uint32_t i = perm2[(it & 1u) * kTile + j];
             const uint32_t s = gs_lo(slot, i);
-            const uint32_t e = i + 1u < cnt ? gs_lo(slot, i + 1u) : gs_lo(slot, kTile);
-            const uint32_t len = e - s;
+            /* the DMA clamps at nkeys, so [cnt] holds the end of a partial
+             * tile's last key; a full tile's ends at the end bound, [256] */
+            const uint32_t len = gs_lo(slot, i + 1u) - s;
             const uint32_t pos = s + (uint32_t)delta - (uint32_t)S16;
             uint32_t h;
             if constexpr ((VAR & 8) != 0) {
                 h = pos ^ len; /* DIAGNOSTIC ONLY: the memory pipeline without hashing */
-            } else if (gs_fits(span)) {
+            } else if (fits(span)) {
                 LdsSrc src{reinterpret_cast<const uint32_t *>(slab_buf(it))};
                 h = wg_value<MODE, VAR>(src, pos, len, tab, tab, dist);
             } else {
@@ -1211,16 +1334,29 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__res
                 h = wg_value<MODE, VAR>(src, S16 + pos, len, tab, tab, dist);
                 __builtin_amdgcn_s_waitcnt(0x0070); /* retire the reader's loads before the paths merge */
             }
-            pend_idx = tile * (uint64_t)kTile + i;
-            pend_h = h;
+            if constexpr (CS) {
+                gs_ds_write_b32(lds_base + G::kRes + (it & 1u) * 4u * kTile + 4u * i, h);
+            } else {
+                pend_idx = tile * (uint64_t)kTile + i;
+                pend_h = h;
+            }
         }
+        pend_tile = tile;
+        pend_cnt = cnt;
+        pend_par = it & 1u;
         if (!more) break;
         tile = t1;
         cnt = cnt1;
         S16 = S16n;
         span = spann;
     }
-    if (pend_idx != ~0ull) out[pend_idx] = pend_h;
+    if constexpr (CS) {
+        full_barrier(); /* every wave's hashes of the last tile are in LDS */
+        store_tile();
+    } else {
+        if (pend_idx != ~0ull) out[pend_idx] = pend_h;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
 }
 
 /* ---------------- register-staged pipeline (variant bit 5) ----------------
@@ -1572,12 +1708,6 @@ struct WrRing {
     static_assert(kWaitSlab <= 63 && kWaitOff <= 63, "vmcnt is 6 bits");
 };
 
-typedef __attribute__((address_space(3))) const void lds_cvoid_t;
-
-__device__ __forceinline__ uint32_t lds_addr(const void *p)
-{
-    return (uint32_t)(uintptr_t)(lds_cvoid_t *)p;
-}
 
 /* LDS-DMA through M0 (saved and restored: M0 is compiler-reserved) */
 template <bool NT>
@@ -1991,6 +2121,7 @@ constexpr int kVarDirectIl32 = (8 | 2) << 20; /* a wave's tiles interleaved over
 constexpr int kVarWsort = 1 << 24; /* the wave-sorted pipeline (nc_wsort_kernels.hip); options in bits 20-23 */
 constexpr int kVarNoFixedLen = 1 << 26; /* md5: no fixed-length specialisation (A/B) */
 constexpr int kVarGsort = 1 << 25; /* the grouped workgroup pipeline (nc_hash_kernel_gs); options in bits 20-23 */
+constexpr int kVarGsortCs = 1 << 27; /* its hashes stored once per tile, 16 bytes per lane */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2117,12 +2248,12 @@ hipError_t launch_mode(const uint8_t *base, const uint64_t *off, uint64_t delta,
 /* One grouped-workgroup launch (variant bit 25): a persistent grid of
  * `sets` resident sets of workgroups (bits 21-22: 6, 1, 3, 8), so
  * workgroups whose tiles ran short hand their slots to new ones. */
-template <int MODE, int VAR>
+template <int MODE, int VAR, int D, bool CS = false>
 hipError_t launch_gs(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                      hipStream_t stream, int var, const WrDist &dist = WrDist{nullptr, 0u, 0u})
 {
     void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist) =
-        nc_hash_kernel_gs<MODE, VAR>;
+        nc_hash_kernel_gs<MODE, VAR, D, CS>;
     static int per_cu = 0;
     if (per_cu == 0) {
         int b = 0;
@@ -2140,15 +2271,23 @@ hipError_t launch_gs(const uint8_t *base, const uint64_t *off, uint64_t delta, u
     return hipGetLastError();
 }
 
-/* bit 20: DIAGNOSTIC no-hash build (fnv1a_64 only; outputs are not hashes) */
+/* bit 20: DIAGNOSTIC no-hash build (fnv1a_64 only; outputs are not hashes);
+ * bit 23: three slab buffers (two slabs in flight) */
 template <int MODE>
 hipError_t launch_gs_mode(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                           hipStream_t stream, int var)
 {
+    const bool d3 = (var & (1 << 23)) != 0;
     if constexpr (MODE == NC_GPUHASH_FNV1A_64) {
-        if (var & (1 << 20)) return launch_gs<MODE, 8>(base, off, delta, nkeys, out, stream, var);
+        if (var & (1 << 20))
+            return d3 ? launch_gs<MODE, 8, 3>(base, off, delta, nkeys, out, stream, var)
+                      : launch_gs<MODE, 8, 2>(base, off, delta, nkeys, out, stream, var);
     }
-    return launch_gs<MODE, 0>(base, off, delta, nkeys, out, stream, var);
+    if (var & kVarGsortCs) /* the previous tile's hashes as one coalesced store */
+        return d3 ? launch_gs<MODE, 0, 3, true>(base, off, delta, nkeys, out, stream, var)
+                  : launch_gs<MODE, 0, 2, true>(base, off, delta, nkeys, out, stream, var);
+    return d3 ? launch_gs<MODE, 0, 3>(base, off, delta, nkeys, out, stream, var)
+              : launch_gs<MODE, 0, 2>(base, off, delta, nkeys, out, stream, var);
 }
 
 /* One wave-ring launch: a persistent grid of every resident workgroup slot
@@ -2404,15 +2543,17 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
      * tiles and oversubscribed grids rebalance that */
     if (mean < 22u) { /* C2 */
         /* the grouped workgroup pipeline (each wave hashes one length
-         * quartile of the tile; its 6 KiB slab holds a 256-key tile up to
-         * ~23 B per key): C2 fnv x4 0.449-0.454 -> 0.429-0.431 ms, hsieh 0.447
-         * -> 0.433, murmur 0.435 -> 0.425, jenkins 0.526 -> 0.445, crc16 0.690
-         * -> 0.645, one_at_a_time 0.504 (wave-sorted) -> 0.473 at three
-         * resident sets (profiles/r03_c2_gsort.jsonl); crc32 / crc32a tie
-         * the workgroup x6 and keep it */
-        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarGsort | (2 << 21);
+         * quartile of the tile; its 6.5 KiB slab holds a 256-key tile up to
+         * ~25 B per key) with one coalesced store per tile: C2 fnv x4
+         * 0.449-0.454 -> 0.429-0.431 ms, hsieh 0.447 -> 0.433, murmur 0.435
+         * -> 0.425, jenkins 0.526 -> 0.445, crc16 0.690 -> 0.645, and the
+         * coalesced store a further 3.5 % on fnv1a_64 (0.452 -> 0.436 on
+         * one box); one_at_a_time 0.504 (wave-sorted) -> 0.476 at three
+         * resident sets (profiles/r03_c2_gsort.jsonl); crc32 / crc32a tie the
+         * workgroup x6 and keep it */
+        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarGsort | kVarGsortCs | (2 << 21);
         if (mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A) return kVarWorkgroup | kVarOver;
-        return kVarGsort;
+        return kVarGsort | kVarGsortCs;
     }
     if (crc || mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarRegStaged | kVarOver;
     return kVarRegStaged;
