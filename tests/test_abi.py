@@ -143,16 +143,17 @@ def test_auto_policy_choices():
     WG, RS, RING5, RING4 = 1 << 16, 32, 128 | (3 << 8), 128
     SORTED, OVER = 1 << 17, 1 << 18
     DIRECT, DIRECT_LDS, IL32 = 1 << 19, 4 << 20, (8 | 2) << 20
-    GSORT, CS = 1 << 25, 1 << 27
+    GSORT, CS, TK512 = 1 << 25, 1 << 27, 1 << 26
     n = 1 << 26
     assert t.pick_variant("fnv1a_64", n) == RS
     assert t.pick_variant("md5", n) == DIRECT  # unknown shape
     # C2 (Zipf 8-64 B, mean 19.3)
-    for name in ("fnv1a_64", "fnv1_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur", "jenkins", "crc16"):
-        assert t.pick_variant(name, n, (19 * n, 8, 64)) == GSORT | CS, name
+    for name in ("fnv1a_64", "fnv1_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur", "jenkins"):
+        assert t.pick_variant(name, n, (19 * n, 8, 64)) == GSORT | CS | TK512 | (2 << 21), name
+    assert t.pick_variant("crc16", n, (19 * n, 8, 64)) == GSORT | CS
     assert t.pick_variant("crc32", n, (19 * n, 8, 64)) == WG | OVER
-    assert t.pick_variant("one_at_a_time", n, (19 * n, 8, 64)) == GSORT | CS | (2 << 21)
-    assert t.pick_variant("one_at_a_time", n, (21 * n, 8, 64)) == GSORT | CS | (2 << 21)
+    assert t.pick_variant("one_at_a_time", n, (19 * n, 8, 64)) == GSORT | CS | TK512
+    assert t.pick_variant("one_at_a_time", n, (21 * n, 8, 64)) == GSORT | CS | TK512
     assert t.pick_variant("md5", n, (19 * n, 8, 64)) == DIRECT
     # uniform 8-64 B (mean 36)
     assert t.pick_variant("fnv1a_64", n, (36 * n, 8, 64)) == RS

@@ -42,7 +42,7 @@ def pools(dist_fixture):
         yield p, len(p["names"])
 
 
-@pytest.mark.parametrize("pipe", [0, 1 << 28, 1 << 29], ids=["policy", "ring", "workgroup"])
+@pytest.mark.parametrize("pipe", [0, 1 << 28, 1 << 29, 1 << 30], ids=["policy", "ring", "workgroup", "grouped"])
 @pytest.mark.parametrize("wide", [False, True], ids=["narrow", "wide"])
 @pytest.mark.parametrize("tag", [None, b"{}", b"::"], ids=["notag", "braces", "colons"])
 def test_server_idx_matches_oracle(gpu, oracle, dist_fixture, tag, wide, pipe):
@@ -185,7 +185,7 @@ def test_device_continuum_end_to_end(gpu, oracle):
     np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want)
 
 
-@pytest.mark.parametrize("pipe", [0, 1 << 28, 1 << 29], ids=["policy", "ring", "workgroup"])
+@pytest.mark.parametrize("pipe", [0, 1 << 28, 1 << 29, 1 << 30], ids=["policy", "ring", "workgroup", "grouped"])
 @pytest.mark.parametrize("tag", [b"::", b"()", b"$$", b"{}", b"ab", b"\x00\x01"], ids=["colons", "parens", "dollars",
                                                                                       "braces", "ab", "nul01"])
 def test_hash_tag_neighbour_bytes(gpu, oracle, dist_fixture, tag, pipe):
@@ -216,5 +216,44 @@ def test_hash_tag_neighbour_bytes(gpu, oracle, dist_fixture, tag, pipe):
                 want = oracle.server_idx_batch(m, 0, kvals, kidx, nserver, tag, keys, off)
                 np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want,
                                               err_msg=f"tag={tag} {t.HASH_NAMES[m]} nserver={nserver}")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
+def test_ketama_lookup_table(gpu, oracle, dist_fixture):
+    """ketama on the grouped pipeline, with the 65536-entry lookup table
+    (variant bit 24, A/B) and without, and the policy's choice, on batches of
+    64 Ki keys and more: every reference-built pool, a synthetic pool of 300
+    servers (48,000 points, past 2^15) and one whose points crowd a few
+    16-bit ranges, hash tags, against the oracle's server_pool_idx."""
+    import torch
+
+    from twemproxy_amd import _lib as L
+
+    spec = t.CONFIGS["C2"]["spec"]
+    n = (1 << 17) + 3
+    keys, off = t.synth_host(spec, 11, n)
+    kd, od = to_dev(keys, off)
+    shape = spec.shape(int(off[-1]))
+    pools = [(np.array(p["ketama"]["values"], np.uint32), np.array(p["ketama"]["indices"], np.uint32), len(p["names"]))
+             for p in dist_fixture["pools"]]
+    rng = np.random.default_rng(3)
+    big = np.sort(rng.integers(0, 1 << 32, size=48000, dtype=np.uint64)).astype(np.uint32)
+    pools.append((big, rng.integers(0, 300, size=big.size).astype(np.uint32), 300))
+    crowd = np.sort(np.concatenate([rng.integers(0, 1 << 18, size=700), rng.integers(0xfffc0000, 1 << 32, size=700),
+                                    rng.integers(0, 1 << 32, size=40)]).astype(np.uint64)).astype(np.uint32)
+    pools.append((crowd, rng.integers(0, 9, size=crowd.size).astype(np.uint32), 9))
+    try:
+        for vals, idx, nserver in pools:
+            cd = t.continuum_device(idx, vals)
+            for m in (6, 1, 10):
+                for tag in (None, b"{}"):
+                    want = oracle.server_idx_batch(m, 0, vals, idx, nserver, tag, keys, off)
+                    for var in ((1 << 30) | (1 << 24), 1 << 30, 0):  # grouped + table, grouped, policy
+                        L.lib().nc_gpuhash_set_tuning(0, 0, var)
+                        got = t.server_idx_device(m, "ketama", kd, od, cd, nserver, hash_tag=tag, shape=shape)
+                        torch.cuda.synchronize()
+                        np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want,
+                                                      err_msg=f"{t.HASH_NAMES[m]} tag={tag} nserver={nserver} {var}")
     finally:
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)

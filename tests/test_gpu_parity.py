@@ -46,7 +46,8 @@ def gpu_hash(mode, keys_d, off_d):
                         (0, 0, (1 << 19) | (14 << 20)), (0, 0, 1 << 24), (0, 0, (1 << 24) | (9 << 20)),
                         (0, 0, 1 << 25), (37, 0, 1 << 25), (0, 0, (1 << 25) | (1 << 21)),
                         (0, 0, (1 << 25) | (1 << 23)), (11, 0, (1 << 25) | (1 << 23) | (2 << 21)),
-                        (0, 0, (1 << 25) | (1 << 27))],
+                        (0, 0, (1 << 25) | (1 << 27)), (0, 0, (1 << 25) | (1 << 27) | (1 << 26)),
+                        (13, 0, (1 << 25) | (1 << 27) | (1 << 26))],
                 ids=["persistent+sort", "auto", "workgroup", "grid37+sort+shiftadd", "shiftadd", "grid5+sort",
                      "sorted_bit", "regstage", "regstage+sort", "grid11+regstage+sort+shiftadd", "grid9+regstage",
                      "cached", "cached+sort", "regstage+cached", "grid7+regstage+cached+sort", "wavering",
@@ -55,7 +56,8 @@ def gpu_hash(mode, keys_d, off_d):
                      "wavering_t64_w4", "wavering_t256_sorted", "grid7+wavering_t256_sorted_w4_6_2_3",
                      "wavering_t256_sorted_5_1_2", "workgroup_over3", "regstage+sort+over3", "direct",
                      "direct_lines", "direct_il32", "direct_lines_il32", "wsort", "wsort_il4",
-                     "gsort", "grid37+gsort", "gsort_1set", "gsort_d3", "grid11+gsort_d3_3sets", "gsort_cs"])
+                     "gsort", "grid37+gsort", "gsort_1set", "gsort_d3", "grid11+gsort_d3_3sets", "gsort_cs", "gsort512",
+                     "grid13+gsort512"])
 def tuning(request):
     grid, sort, var = request.param
     L.lib().nc_gpuhash_set_tuning(grid, sort, var)
@@ -245,7 +247,8 @@ def test_sort_and_grid_variants_agree_full_size(gpu):
                             (0, 0, 1 << 25), (1, 0, 1 << 25), (4096, 0, 1 << 25), (0, 0, (1 << 25) | (3 << 21)),
                             (0, 0, (1 << 25) | (1 << 23)), (1, 0, (1 << 25) | (1 << 23)),
                             (777, 0, (1 << 25) | (1 << 23)), (0, 0, (1 << 25) | (1 << 27)),
-                            (0, 0, (1 << 25) | (1 << 23) | (1 << 27))):
+                            (0, 0, (1 << 25) | (1 << 23) | (1 << 27)), (0, 0, (1 << 25) | (1 << 27) | (1 << 26)),
+                            (1, 0, (1 << 25) | (1 << 27) | (1 << 26))):
         L.lib().nc_gpuhash_set_tuning(grid, sort, var)
         out = t.hash_batch_device("fnv1a_64", kd, od)
         torch.cuda.synchronize()
@@ -466,8 +469,10 @@ def test_wsort_round_of_long_keys(gpu, oracle, var):
 @pytest.mark.parametrize("tune", [(0, 1 << 25), (0, (1 << 25) | (1 << 21)), (3, 1 << 25), (1, (1 << 25) | (3 << 21)),
                                   (0, (1 << 25) | (1 << 23)), (2, (1 << 25) | (1 << 23)),
                                   (0, (1 << 25) | (1 << 23) | (1 << 21)), (0, (1 << 25) | (1 << 27)),
-                                  (5, (1 << 25) | (1 << 23) | (1 << 27))],
-                         ids=["gsort6", "gsort1", "grid3", "grid1_8sets", "d3", "d3_grid2", "d3_1set", "cs", "d3_cs_grid5"])
+                                  (5, (1 << 25) | (1 << 23) | (1 << 27)), (0, (1 << 25) | (1 << 27) | (1 << 26)),
+                                  (2, (1 << 25) | (1 << 27) | (1 << 26) | (1 << 21))],
+                         ids=["gsort6", "gsort1", "grid3", "grid1_8sets", "d3", "d3_grid2", "d3_1set", "cs", "d3_cs_grid5",
+                              "tk512", "tk512_grid2"])
 def test_gsort_ragged_tiles(gpu, oracle, tune):
     """The grouped workgroup pipeline (variant bit 25: offsets by LDS-DMA two
     tiles ahead, wave 0 sorting the next tile, each wave one length quartile)
@@ -523,7 +528,7 @@ def test_virtual_key_base(gpu, oracle):
         out = torch.empty(n, dtype=torch.int32, device="cuda")
         shape = L.NcShape(int(off[-1]), *spec.len_range())
         for var in (0, 65536, 32, 128, 896, 1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (14 << 20), 1 << 24,
-                    1 << 25, (1 << 25) | (1 << 23), (1 << 25) | (1 << 27)):
+                    1 << 25, (1 << 25) | (1 << 23), (1 << 25) | (1 << 27), (1 << 25) | (1 << 27) | (1 << 26)):
             L.lib().nc_gpuhash_set_tuning(0, 0, var)
             try:
                 for m in MODES:

@@ -79,7 +79,8 @@ def test_no_scratch_in_hash_kernels(asm_file):
 
 def test_lds_fits_eight_workgroups(asm_file):
     """Every workgroup-pipeline kernel leaves room for eight workgroups per
-    CU (160 KiB of LDS), the grouped pipeline's three-slab form for seven."""
+    CU (160 KiB of LDS), the grouped pipeline's three-slab form for seven
+    and its eight-wave (512-key) form for four."""
     text = open(asm_file).read()
     for block in text.split(".amdhsa_kernel ")[1:]:
         name = block.split()[0]
@@ -88,6 +89,8 @@ def test_lds_fits_eight_workgroups(asm_file):
         lds = int([l for l in block.splitlines() if ".amdhsa_group_segment_fixed_size" in l][0].split()[-1])
         # the grouped pipeline's three-slab form (nc_hash_kernel_gs<.., D = 3, ..>) is sized for seven
         per_cu = 7 if "nc_hash_kernel_gs" in name and "ELi3ELb" in name else 8
+        if "nc_hash_kernel_gs" in name and "ELi512E" in name:  # eight-wave workgroups: four per CU
+            per_cu = 4
         assert lds * per_cu <= 160 * 1024, (name, lds)
 
 

@@ -13,7 +13,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
-PIPES = {"policy": 0, "ring": 1 << 28, "workgroup": 1 << 29}
+PIPES = {"policy": 0, "ring": 1 << 28, "workgroup": 1 << 29, "grouped": 1 << 30, "grouped3": (1 << 30) | (2 << 21),
+         "grouped1": (1 << 30) | (1 << 21), "grouped_lut": (1 << 30) | (1 << 24)}
 GRIDS = {}  # name -> grid cap (--grids: workgroup pipeline at these caps)
 
 

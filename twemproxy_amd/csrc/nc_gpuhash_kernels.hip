@@ -538,14 +538,31 @@ __device__ __forceinline__ void full_barrier()
     asm volatile("" ::: "memory");
 }
 
-constexpr int kDistNone = -1, kDistKetama = 0, kDistModula = 1, kDistPre = 3;
+constexpr int kDistNone = -1, kDistKetama = 0, kDistModula = 1, kDistPre = 3, kDistKetamaLut = 4;
 
 /* server_pool_idx parameters of one launch (ignored for kDistNone) */
 struct WrDist {
     const uint32_t *cont; /* struct continuum {index, value} pairs (src/nc_server.h:64-67) */
     uint32_t ncont;
     uint32_t tag;         /* hash_tag c0 | c1 << 8 | 1 << 16, or 0 for none */
+    const uint32_t *lut;  /* ketama lookup table by the hash's top 16 bits (kDistKetamaLut), or null */
 };
+
+/* ketama_dispatch through a 65536-entry table over the hash's top 16 bits
+ * (nc_ketama_lut_kernel): an entry without bit 31 is the server of every
+ * hash in its range (no point falls inside the range), else it names the
+ * first point >= the range start and the answer is the first point >= h from
+ * there (src/hashkit/nc_ketama.c:222-246: the first value >= hash, wrapping
+ * to the first point). One L2 read per key for ~98 % of keys of an 8-server
+ * pool, instead of a binary search of dependent reads. */
+__device__ __forceinline__ uint32_t ketama_find_lut(const uint32_t *c, const uint32_t *lut, uint32_t n, uint32_t h)
+{
+    const uint32_t e = lut[h >> 16];
+    if ((e >> 31) == 0u) return e;
+    uint32_t p = e & 0x7fffffffu;
+    while (p < n && c[2u * p + 1u] < h) p++;
+    return c[2u * (p == n ? 0u : p)];
+}
 
 /* hash_tag trimming of server_pool_idx (src/nc_server.c:665-677): the first
  * c0, then the first c1 after it; with at least one byte between them the
@@ -660,7 +677,10 @@ __device__ __forceinline__ uint32_t cont_lower_bound(const uint32_t *c, uint32_t
 template <int VAR>
 constexpr int wg_dist()
 {
-    return ((VAR >> 12) & 3) == 1 ? kDistKetama : ((VAR >> 12) & 3) == 2 ? kDistModula : kDistNone;
+    return ((VAR >> 12) & 3) == 1   ? kDistKetama
+           : ((VAR >> 12) & 3) == 2 ? kDistModula
+           : ((VAR >> 12) & 3) == 3 ? kDistKetamaLut
+                                    : kDistNone;
 }
 
 template <int MODE, int VAR, class Src>
@@ -678,6 +698,8 @@ __device__ __forceinline__ uint32_t wg_value(const Src &src, typename Src::pos_t
         const uint32_t n = dist.ncont;
         if constexpr (D == kDistModula) {
             return c[2u * (h % n)]; /* nc_modula.c:153 */
+        } else if constexpr (D == kDistKetamaLut) {
+            return ketama_find_lut(c, dist.lut, n, h);
         } else { /* ketama_dispatch, nc_ketama.c:222-246 */
             const uint32_t b = h >> 24;
             uint32_t lo = bkt[b];
@@ -1038,65 +1060,78 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p)
 
 /* ---------------- grouped workgroup pipeline (variant bit 25) ----------------
  *
- * The workgroup pipeline's tiles (256 keys, 4 waves, LDS-DMA slabs, one
- * barrier per tile), with each WAVE hashing one length quartile of the tile
- * instead of 64 neighbouring keys: a wave runs as long as its longest key,
- * so under Zipf 8-64 B four unsorted waves cost ~4 x 61 byte steps per tile,
- * four length-grouped ones ~110. The grouping costs no barrier: a tile's
- * offsets arrive by LDS-DMA D tiles ahead (the whole workgroup sees them
- * after a top barrier), and wave 0 — which hashes the shortest quartile —
- * counting-sorts tile t+1 while the others hash tile t, leaving the
- * permutation in LDS for the next iteration. Offsets are read from HBM once,
- * the low dword of each (lengths and slab positions are 32-bit; the tile
- * bounds' high dwords come separately).
+ * The workgroup pipeline's tiles (TK keys, TK/64 waves, LDS-DMA slabs, one
+ * barrier per tile), with each WAVE hashing one length group of the tile
+ * (its 64 keys of one rank range) instead of 64 neighbouring keys: a wave
+ * runs as long as its longest key, so under Zipf 8-64 B unsorted waves cost
+ * ~61 byte steps each, length-grouped ones ~110 per 256 keys in all (TK =
+ * 256, four quartiles) or ~92 (TK = 512, eight octiles). The grouping costs
+ * no barrier: a tile's offsets arrive by LDS-DMA D tiles ahead (the whole
+ * workgroup sees them after a top barrier), and wave 0 — which hashes the
+ * shortest group — counting-sorts tile t+1 while the others hash tile t,
+ * leaving the permutation in LDS for the next iteration. Offsets are read
+ * from HBM once, the low dword of each (lengths and slab positions are
+ * 32-bit; the tile bounds' high dwords come separately).
  *
- * D = 2: slab(t+1) in flight while tile t hashes (8 workgroups per CU, the
- * top barrier waits for everything). D = 3: slabs t+1 and t+2 in flight (7
- * workgroups per CU): every wave issues exactly kSlabIters slab DMAs per
- * tile (dummies where a slab needs fewer), so the top barrier waits with a
- * counted vmcnt that leaves the youngest slab in flight; the sorter's LDS
- * writes are inline asm, which hipcc does not hold behind that DMA.
+ * D = 2: slab(t+1) in flight while tile t hashes (the top barrier waits for
+ * everything). D = 3: slabs t+1 and t+2 in flight: every wave issues exactly
+ * kSlabIters slab DMAs per tile (dummies where a slab needs fewer), so the
+ * top barrier waits with a counted vmcnt that leaves the youngest slab in
+ * flight. Every LDS access hipcc could hold behind an in-flight LDS-DMA (a
+ * write, or a read it cannot prove disjoint) is inline asm. CS: a tile's
+ * hashes go to LDS by key index and out as 16-byte-per-lane stores.
  *
  * Iteration t (after the top barrier: slab(t), offsets(t+1 .. t+D-1) and
- * perm(t) in LDS): pending stores of tile t-1; wave 0 sorts tile t+1; DMA
- * offsets(t+D) and slab(t+D-1); every wave hashes its quartile of tile t. */
-template <int D, bool CS>
+ * perm(t) in LDS): pending stores of tile t-1; DMA offsets(t+D) and
+ * slab(t+D-1); wave 0 sorts tile t+1; every wave hashes its group of tile t. */
+template <int D, bool CS, int TK>
 struct GsLds {
     static_assert(D == 2 || D == 3, "two or three slab buffers");
-    static constexpr uint32_t kOffSlot = 1040; /* u32 lo[256], then end lo / hi and start hi */
-    static constexpr uint32_t kNOff = D + 1;    /* offsets of tiles t .. t+D */
-    static constexpr uint32_t kResBytes = CS ? 2u * 4u * kTile : 0u; /* u32[2][256]: hashes by key, for one coalesced store */
-    static constexpr uint32_t kFixed = kNOff * kOffSlot + 2 * kTile + 4 * 64 + 4 * 256 + 16 + kResBytes;
-    static constexpr uint32_t kBudget = D == 2 ? 20480 : 23392; /* 8 / 7 workgroups per CU */
+    static_assert(TK == 256 || TK == 512, "four or eight waves");
+    static constexpr uint32_t kOffSlot = 4u * TK + 16u; /* u32 lo[TK], then end lo / hi and start hi */
+    static constexpr uint32_t kNOff = D + 1;             /* offsets of tiles t .. t+D */
+    static constexpr uint32_t kPermBytes = 2u * 2u * TK; /* u16[2][TK]: sorted position -> key index */
+    static constexpr uint32_t kResBytes = CS ? 2u * 4u * TK : 0u; /* u32[2][TK]: hashes by key index */
+    static constexpr uint32_t kFixed = kNOff * kOffSlot + kPermBytes + 4 * 64 + 4 * 256 + 16 + kResBytes;
+    /* 8 / 7 workgroups of four waves per CU; 4 of eight */
+    static constexpr uint32_t kBudget = TK == 512 ? 40960 : (D == 2 ? 20480 : 23392);
     static constexpr uint32_t kCap = ((kBudget - kFixed) / D) & ~15u;
     static constexpr uint32_t kOffs = D * kCap;
-    static constexpr uint32_t kPerm = kOffs + kNOff * kOffSlot; /* u8[2][256]: sorted position -> key index */
-    static constexpr uint32_t kHist = kPerm + 2 * kTile;        /* u32[64], the sorter's counters */
+    static constexpr uint32_t kPerm = kOffs + kNOff * kOffSlot;
+    static constexpr uint32_t kHist = kPerm + kPermBytes;       /* u32[64], the sorter's counters */
     static constexpr uint32_t kTab = kHist + 4 * 64;            /* u32[256]: crc table / ketama bucket index */
     static constexpr uint32_t kDump = kTab + 4 * 256;           /* landing area of dummy DMAs */
     static constexpr uint32_t kRes = kDump + 16;
     static constexpr uint32_t kBytes = kRes + kResBytes;
-    static constexpr int kSlabIters = (int)((kCap / 16 + kBlock - 1) / kBlock);
+    static constexpr int kSlabIters = (int)((kCap / 16 + TK - 1) / TK);
     static_assert(kBytes <= kBudget, "LDS budget");
-    static_assert(kOffs % 16 == 0 && kTab % 16 == 0 && kCap % 16 == 0, "LDS carve must stay 16-byte aligned");
+    static_assert(kOffs % 16 == 0 && kTab % 16 == 0 && kCap % 16 == 0 && kRes % 16 == 0,
+                  "LDS carve must stay 16-byte aligned");
 };
 
-/* low dwords of off[k0 .. k0+255] (clamped at nkeys) into slot, one 4-byte
+template <int TK>
+__device__ __forceinline__ uint32_t gs_tile_count(uint64_t tile, uint64_t nkeys)
+{
+    const uint64_t left = nkeys - tile * (uint64_t)TK;
+    return left < (uint64_t)TK ? (uint32_t)left : (uint32_t)TK;
+}
+
+/* low dwords of off[k0 .. k0+TK-1] (clamped at nkeys) into slot, one 4-byte
  * DMA per lane; wave 0 adds the end bound off[k0+cnt] (low, high) and the
- * start's high dword at [256..258] */
-template <int AUX>
+ * start's high dword at [TK .. TK+2] */
+template <int AUX, int TK>
 __device__ __forceinline__ void gs_issue_offs(const uint64_t *__restrict__ off, uint64_t tile, uint64_t nkeys,
                                               uint8_t *slot, uint32_t t)
 {
-    const uint64_t k0 = tile * (uint64_t)kTile;
+    const uint64_t k0 = tile * (uint64_t)TK;
     uint64_t k = k0 + t;
     if (k > nkeys) k = nkeys;
     const uint32_t *o32 = reinterpret_cast<const uint32_t *>(off);
     __builtin_amdgcn_global_load_lds((gbl_void_t *)(o32 + 2u * k), (lds_void_t *)(slot + 4u * (t & ~63u)), 4, 0, AUX);
     if (t < 3u) {
-        const uint64_t e = k0 + tile_count(tile, nkeys);
+        const uint64_t e = k0 + gs_tile_count<TK>(tile, nkeys);
         const uint32_t *src = t == 0u ? o32 + 2u * e : t == 1u ? o32 + 2u * e + 1u : o32 + 2u * k0 + 1u;
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)src, (lds_void_t *)(slot + 4u * kTile), 4, 0, AUX);
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)src, (lds_void_t *)(slot + 4u * TK), 4, 0, AUX);
     }
 }
 
@@ -1114,9 +1149,9 @@ __device__ __forceinline__ void gs_ds_write_b32(uint32_t a, uint32_t v)
 {
     asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
-__device__ __forceinline__ void gs_ds_write_b8(uint32_t a, uint32_t v)
+__device__ __forceinline__ void gs_ds_write_b16(uint32_t a, uint32_t v)
 {
-    asm volatile("ds_write_b8 %0, %1" ::"v"(a), "v"(v) : "memory");
+    asm volatile("ds_write_b16 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
 __device__ __forceinline__ uint32_t gs_ds_add_rtn(uint32_t a, uint32_t v)
 {
@@ -1131,27 +1166,35 @@ __device__ __forceinline__ uint32_t gs_ds_read_b32(uint32_t a)
     return r;
 }
 
-/* counting sort of the tile in `slot` by length class (one wave): perm[pos]
- * = key index, ascending classes; absent keys (>= cnt) last (class 63;
- * valid keys clamp to 62). hist / perm are LDS byte addresses. */
+/* counting sort of the tile in `slot` by length class (one wave, KPL = TK/64
+ * keys per lane): perm[pos] = key index (u16), ascending classes; absent
+ * keys (>= cnt) last (class 63; valid keys clamp to 62). hist / perm are
+ * LDS byte addresses. */
+template <int TK>
 __device__ __forceinline__ void gs_sort(const uint8_t *slot, uint32_t cnt, uint32_t hist, uint32_t perm, uint32_t lane)
 {
+    constexpr int KPL = TK / 64;
     gs_ds_write_b32(hist + 4u * lane, 0u);
-    const uint32_t sa = lds_addr(slot) + 16u * lane;
-    uint32_t st[5];
+    const uint32_t sa = lds_addr(slot) + 4u * KPL * lane;
+    uint32_t st[KPL + 1];
 #pragma unroll
-    for (int q = 0; q < 5; q++) st[q] = gs_ds_read_b32(sa + 4u * (uint32_t)q); /* [256] is lane 63's end bound */
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(st[0]), "+v"(st[1]), "+v"(st[2]), "+v"(st[3]), "+v"(st[4])::"memory");
-    uint32_t cls[4], rk[4];
+    for (int q = 0; q <= KPL; q++) st[q] = gs_ds_read_b32(sa + 4u * (uint32_t)q); /* [TK] is lane 63's end bound */
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const uint32_t i = 4u * lane + (uint32_t)q;
-        const uint32_t len = st[q + 1] - st[q]; /* key 255 ends at the end bound, [256] */
+    for (int q = 0; q <= KPL; q++) asm volatile("" : "+v"(st[q]));
+    uint32_t cls[KPL], rk[KPL];
+#pragma unroll
+    for (int q = 0; q < KPL; q++) {
+        const uint32_t i = (uint32_t)KPL * lane + (uint32_t)q;
+        const uint32_t len = st[q + 1] - st[q];
         cls[q] = i < cnt ? (len < 62u ? len : 62u) : 63u;
         rk[q] = gs_ds_add_rtn(hist + 4u * cls[q], 1u);
     }
     uint32_t c = gs_ds_read_b32(hist + 4u * lane);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rk[0]), "+v"(rk[1]), "+v"(rk[2]), "+v"(rk[3]), "+v"(c)::"memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int q = 0; q < KPL; q++) asm volatile("" : "+v"(rk[q]));
+    asm volatile("" : "+v"(c));
     uint32_t incl = c;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -1159,24 +1202,26 @@ __device__ __forceinline__ void gs_sort(const uint8_t *slot, uint32_t cnt, uint3
         if (lane >= (uint32_t)d) incl += v;
     }
     gs_ds_write_b32(hist + 4u * lane, incl - c);
-    uint32_t b[4];
+    uint32_t b[KPL];
 #pragma unroll
-    for (int q = 0; q < 4; q++) b[q] = gs_ds_read_b32(hist + 4u * cls[q]);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
+    for (int q = 0; q < KPL; q++) b[q] = gs_ds_read_b32(hist + 4u * cls[q]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int q = 0; q < 4; q++) gs_ds_write_b8(perm + b[q] + rk[q], 4u * lane + (uint32_t)q);
+    for (int q = 0; q < KPL; q++) asm volatile("" : "+v"(b[q]));
+#pragma unroll
+    for (int q = 0; q < KPL; q++) gs_ds_write_b16(perm + 2u * (b[q] + rk[q]), (uint32_t)KPL * lane + (uint32_t)q);
 }
 
-template <int MODE, int VAR, int D, bool CS>
-__global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__restrict__ keys_base,
-                                                            const uint64_t *__restrict__ off, uint64_t delta,
-                                                            uint64_t nkeys, uint32_t *__restrict__ out,
-                                                            uint64_t ntiles, WrDist dist)
+template <int MODE, int VAR, int D, bool CS, int TK>
+__global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restrict__ keys_base,
+                                                        const uint64_t *__restrict__ off, uint64_t delta,
+                                                        uint64_t nkeys, uint32_t *__restrict__ out, uint64_t ntiles,
+                                                        WrDist dist)
 {
-    using G = GsLds<D, CS>;
+    using G = GsLds<D, CS, TK>;
     constexpr int kAux = 2; /* nt: read-once streams */
     __shared__ __attribute__((aligned(16))) uint8_t smem[G::kBytes];
-    const uint8_t *perm2 = smem + G::kPerm;
+    const uint16_t *perm2 = reinterpret_cast<const uint16_t *>(smem + G::kPerm);
     uint32_t *tab = reinterpret_cast<uint32_t *>(smem + G::kTab);
     const uint32_t lds_base = lds_addr(smem);
 
@@ -1194,13 +1239,14 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__res
         return smem + G::kOffs + (it % G::kNOff) * G::kOffSlot;
     };
     auto slab_buf = [&](uint32_t it) __attribute__((always_inline)) { return smem + (it % (uint32_t)D) * G::kCap; };
-    /* the slab of the tile whose offsets are in `slot`: its 16-aligned start and span */
-    /* (inline-asm reads: hipcc would hold a plain LDS read of a slot behind
-     * the slab DMA in flight, vmcnt(0), not knowing the two are disjoint) */
+    /* the slab of the tile whose offsets are in `slot`: its 16-aligned start
+     * and span (inline-asm reads: hipcc would hold a plain LDS read of a slot
+     * behind the slab DMA in flight, vmcnt(0), not knowing the two are
+     * disjoint) */
     auto bounds = [&](const uint8_t *slot, uint64_t &S16, uint64_t &span) __attribute__((always_inline)) {
         const uint32_t a = lds_addr(slot);
-        uint32_t s_lo = gs_ds_read_b32(a), e_lo = gs_ds_read_b32(a + 4u * kTile);
-        uint32_t e_hi = gs_ds_read_b32(a + 4u * kTile + 4u), s_hi = gs_ds_read_b32(a + 4u * kTile + 8u);
+        uint32_t s_lo = gs_ds_read_b32(a), e_lo = gs_ds_read_b32(a + 4u * TK);
+        uint32_t e_hi = gs_ds_read_b32(a + 4u * TK + 4u), s_hi = gs_ds_read_b32(a + 4u * TK + 8u);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(s_lo), "+v"(e_lo), "+v"(e_hi), "+v"(s_hi)::"memory");
         const uint64_t S = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(s_hi) << 32) |
                             (uint32_t)__builtin_amdgcn_readfirstlane(s_lo)) + delta;
@@ -1217,12 +1263,12 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__res
         const uint32_t wbase = t & ~63u;
 #pragma unroll
         for (int i = 0; i < G::kSlabIters; i++) {
-            const uint32_t c = t + (uint32_t)i * kBlock;
-            if (wbase + (uint32_t)i * kBlock < nch) {
+            const uint32_t c = t + (uint32_t)i * TK;
+            if (wbase + (uint32_t)i * TK < nch) {
                 if (c < nch)
                     __builtin_amdgcn_global_load_lds((gbl_void_t *)(keys_base + S16 + 16u * c),
-                                                     (lds_void_t *)(buf + 16u * (wbase + (uint32_t)i * kBlock)), 16,
-                                                     0, kAux);
+                                                     (lds_void_t *)(buf + 16u * (wbase + (uint32_t)i * TK)), 16, 0,
+                                                     kAux);
             } else if (D == 3 && lane == 0u) {
                 __builtin_amdgcn_global_load_lds((gbl_void_t *)(off + nkeys), (lds_void_t *)(smem + G::kDump), 4, 0,
                                                  0);
@@ -1242,15 +1288,18 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__res
         }
     };
 
-    if constexpr (uses_crc_table<MODE>()) tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
-    if constexpr (wg_dist<VAR>() == kDistKetama) tab[t] = cont_lower_bound(dist.cont, dist.ncont, t << 24);
+    if (t < 256u) {
+        if constexpr (uses_crc_table<MODE>())
+            tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
+        if constexpr (wg_dist<VAR>() == kDistKetama) tab[t] = cont_lower_bound(dist.cont, dist.ncont, t << 24);
+    }
 
     /* prologue: offsets of tiles 0 .. D-1; perm(0); slabs 0 .. D-2 */
 #pragma unroll
-    for (uint32_t j = 0; j < (uint32_t)D; j++) gs_issue_offs<kAux>(off, tile_at(j), nkeys, offs_slot(j), t);
+    for (uint32_t j = 0; j < (uint32_t)D; j++) gs_issue_offs<kAux, TK>(off, tile_at(j), nkeys, offs_slot(j), t);
     full_barrier();
-    uint32_t cnt = tile_count(tile, nkeys);
-    if (wave == 0u) gs_sort(offs_slot(0), cnt, lds_base + G::kHist, lds_base + G::kPerm, lane);
+    uint32_t cnt = gs_tile_count<TK>(tile, nkeys);
+    if (wave == 0u) gs_sort<TK>(offs_slot(0), cnt, lds_base + G::kHist, lds_base + G::kPerm, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     uint64_t S16, span;
     bounds(offs_slot(0), S16, span);
@@ -1263,20 +1312,21 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__res
 
     uint64_t pend_idx = ~0ull;
     uint32_t pend_h = 0;
-    /* CS: the previous tile's hashes, left in LDS by key index, go out as one
-     * 16-byte-per-lane store of wave 1 (a partial or misaligned tile: one
-     * dword per thread) */
+    /* CS: the previous tile's hashes, left in LDS by key index, go out as
+     * 16-byte-per-lane stores, one wave per 256 keys (a partial or misaligned
+     * tile: one dword per thread) */
     uint64_t pend_tile = ~0ull;
     uint32_t pend_cnt = 0, pend_par = 0;
     const bool out16 = (reinterpret_cast<uintptr_t>(out) & 15u) == 0u;
     auto store_tile = [&]() __attribute__((always_inline)) {
-        const uint32_t ra = lds_base + G::kRes + pend_par * 4u * kTile;
-        uint32_t *dst = out + pend_tile * (uint64_t)kTile;
-        if (pend_cnt == kTile && out16) {
-            if (wave == 1u) {
+        const uint32_t ra = lds_base + G::kRes + pend_par * 4u * TK;
+        uint32_t *dst = out + pend_tile * (uint64_t)TK;
+        if (pend_cnt == (uint32_t)TK && out16) {
+            if (wave >= 1u && wave <= (uint32_t)TK / 256u) {
+                const uint32_t q = 64u * (wave - 1u) + lane; /* 16-byte piece */
                 gs_u32x4 v;
-                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ra + 16u * lane) : "memory");
-                __builtin_nontemporal_store(v, reinterpret_cast<gs_u32x4 *>(dst) + lane);
+                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ra + 16u * q) : "memory");
+                __builtin_nontemporal_store(v, reinterpret_cast<gs_u32x4 *>(dst) + q);
             }
         } else if (t < pend_cnt) {
             uint32_t v;
@@ -1295,32 +1345,31 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__res
         asm volatile("" ::: "memory");
         const uint64_t t1 = tile + stride;
         const bool more = t1 < ntiles;
-        const uint32_t cnt1 = more ? tile_count(t1, nkeys) : 0u;
+        const uint32_t cnt1 = more ? gs_tile_count<TK>(t1, nkeys) : 0u;
         /* every LDS read of the offsets slots comes before this iteration's
-         * DMAs: hipcc waits vmcnt(0) before an LDS read it cannot prove
-         * disjoint from an LDS-DMA in flight */
+         * DMAs */
         uint64_t S16n = 0, spann = 0, sn, pn;
         if (more) bounds(offs_slot(it + 1u), S16n, spann);
         bounds(offs_slot(it + (uint32_t)D - 1u), sn, pn); /* slab(t + D - 1) */
         const bool dn = tile + (uint64_t)(D - 1) * stride < ntiles && fits(pn);
-        gs_issue_offs<kAux>(off, tile_at(D), nkeys, offs_slot(it + (uint32_t)D), t);
+        gs_issue_offs<kAux, TK>(off, tile_at(D), nkeys, offs_slot(it + (uint32_t)D), t);
         slab_dma(dn, sn, pn, slab_buf(it + (uint32_t)D - 1u));
         asm volatile("" ::: "memory");
         /* wave 0 sorts tile t+1 with its DMAs already out (every LDS access
          * of the sort is inline asm, which hipcc does not hold behind them) */
         if (more && wave == 0u)
-            gs_sort(offs_slot(it + 1u), cnt1, lds_base + G::kHist, lds_base + G::kPerm + ((it + 1u) & 1u) * kTile,
-                    lane);
+            gs_sort<TK>(offs_slot(it + 1u), cnt1, lds_base + G::kHist, lds_base + G::kPerm + ((it + 1u) & 1u) * 2u * TK,
+                        lane);
         asm volatile("" ::: "memory");
 
-        /* this wave's length quartile of tile `tile` */
+        /* this wave's length group of tile `tile` */
         const uint8_t *slot = offs_slot(it);
         const uint32_t j = 64u * wave + lane;
         if (j < cnt) {
-            const uint32_t i = perm2[(it & 1u) * kTile + j];
+            const uint32_t i = perm2[(it & 1u) * TK + j];
             const uint32_t s = gs_lo(slot, i);
             /* the DMA clamps at nkeys, so [cnt] holds the end of a partial
-             * tile's last key; a full tile's ends at the end bound, [256] */
+             * tile's last key; a full tile's ends at the end bound, [TK] */
             const uint32_t len = gs_lo(slot, i + 1u) - s;
             const uint32_t pos = s + (uint32_t)delta - (uint32_t)S16;
             uint32_t h;
@@ -1335,9 +1384,9 @@ __global__ __launch_bounds__(kBlock) void nc_hash_kernel_gs(const uint8_t *__res
                 __builtin_amdgcn_s_waitcnt(0x0070); /* retire the reader's loads before the paths merge */
             }
             if constexpr (CS) {
-                gs_ds_write_b32(lds_base + G::kRes + (it & 1u) * 4u * kTile + 4u * i, h);
+                gs_ds_write_b32(lds_base + G::kRes + (it & 1u) * 4u * TK + 4u * i, h);
             } else {
-                pend_idx = tile * (uint64_t)kTile + i;
+                pend_idx = tile * (uint64_t)TK + i;
                 pend_h = h;
             }
         }
@@ -2017,6 +2066,19 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
 }
 
+/* the ketama lookup table (ketama_find_lut): one thread per 16-bit range */
+__global__ __launch_bounds__(256) void nc_ketama_lut_kernel(const uint32_t *__restrict__ cont, uint32_t n,
+                                                            uint32_t *__restrict__ lut)
+{
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    if (b >= 65536u) return;
+    const uint32_t lo = b << 16, hi = lo | 0xffffu;
+    const uint32_t p = cont_lower_bound(cont, n, lo);
+    if (p == n) lut[b] = cont[0];                             /* every hash here wraps to the first point */
+    else if (cont[2u * p + 1u] > hi) lut[b] = cont[2u * p];   /* no point inside: one server for the range */
+    else lut[b] = 0x80000000u | p;
+}
+
 /* ketama / modula over pre-dispatch hashes, in place (continua too large
  * for the fused kernel's LDS); the continuum is read through L2 */
 template <int DIST>
@@ -2068,6 +2130,9 @@ struct DistArgs {
     int kind;
     bool wide; /* 5 KiB slab slots two tiles ahead (keys of 20+ B) instead of 3 KiB one ahead */
     bool wg;   /* the workgroup pipeline (continuum in L2, bucket index in LDS) instead of the wave ring */
+    bool gs;   /* the grouped workgroup pipeline (one length quartile per wave), continuum as for wg */
+    int gs_var; /* its launch options (variant bits 21-22: resident sets) */
+    const uint32_t *lut; /* ketama lookup table (ketama_find_lut) for the grouped pipeline, or null */
 };
 /* fused hash -> dispatch of mode MODE on the wave ring (offsets 16-byte aligned) */
 template <int MODE>
@@ -2122,6 +2187,7 @@ constexpr int kVarWsort = 1 << 24; /* the wave-sorted pipeline (nc_wsort_kernels
 constexpr int kVarNoFixedLen = 1 << 26; /* md5: no fixed-length specialisation (A/B) */
 constexpr int kVarGsort = 1 << 25; /* the grouped workgroup pipeline (nc_hash_kernel_gs); options in bits 20-23 */
 constexpr int kVarGsortCs = 1 << 27; /* its hashes stored once per tile, 16 bytes per lane */
+constexpr int kVarGsort512 = 1 << 26; /* with kVarGsortCs: 512-key tiles, eight waves (length octiles) */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2165,7 +2231,7 @@ int num_cus()
 
 template <int MODE, bool SORT, int VAR>
 hipError_t launch_kernel(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
-                         hipStream_t stream, int var, const WrDist &dist = WrDist{nullptr, 0u, 0u})
+                         hipStream_t stream, int var, const WrDist &dist = WrDist{nullptr, 0u, 0u, nullptr})
 {
     /* persistent grid: every resident workgroup slot once (occupancy query
      * cached per instantiation), unless a cap is set */
@@ -2248,26 +2314,25 @@ hipError_t launch_mode(const uint8_t *base, const uint64_t *off, uint64_t delta,
 /* One grouped-workgroup launch (variant bit 25): a persistent grid of
  * `sets` resident sets of workgroups (bits 21-22: 6, 1, 3, 8), so
  * workgroups whose tiles ran short hand their slots to new ones. */
-template <int MODE, int VAR, int D, bool CS = false>
+template <int MODE, int VAR, int D, bool CS = false, int TK = 256>
 hipError_t launch_gs(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
-                     hipStream_t stream, int var, const WrDist &dist = WrDist{nullptr, 0u, 0u})
+                     hipStream_t stream, int var, const WrDist &dist = WrDist{nullptr, 0u, 0u, nullptr})
 {
     void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist) =
-        nc_hash_kernel_gs<MODE, VAR, D, CS>;
+        nc_hash_kernel_gs<MODE, VAR, D, CS, TK>;
     static int per_cu = 0;
     if (per_cu == 0) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, kBlock, 0) != hipSuccess || b <= 0) b = 4;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, TK, 0) != hipSuccess || b <= 0) b = 4;
         per_cu = b;
     }
     static const uint64_t kSets[4] = {6, 1, 3, 8};
-    const uint64_t ntiles = (nkeys + kTile - 1) / kTile;
+    const uint64_t ntiles = (nkeys + TK - 1) / TK;
     const int cap = grid_cap();
     uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu * kSets[(var >> 21) & 3];
     if (grid > ntiles) grid = ntiles;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, stream, base, off, delta, nkeys, out, ntiles,
-                       dist);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(TK), 0, stream, base, off, delta, nkeys, out, ntiles, dist);
     return hipGetLastError();
 }
 
@@ -2279,13 +2344,18 @@ hipError_t launch_gs_mode(const uint8_t *base, const uint64_t *off, uint64_t del
 {
     const bool d3 = (var & (1 << 23)) != 0;
     if constexpr (MODE == NC_GPUHASH_FNV1A_64) {
-        if (var & (1 << 20))
+        if (var & (1 << 20)) {
+            if (var & kVarGsortCs) return launch_gs<MODE, 8, 2, true>(base, off, delta, nkeys, out, stream, var);
             return d3 ? launch_gs<MODE, 8, 3>(base, off, delta, nkeys, out, stream, var)
                       : launch_gs<MODE, 8, 2>(base, off, delta, nkeys, out, stream, var);
+        }
     }
-    if (var & kVarGsortCs) /* the previous tile's hashes as one coalesced store */
+    if (var & kVarGsortCs) { /* the previous tile's hashes as one coalesced store */
+        if (var & kVarGsort512) /* 512-key tiles, eight waves, length octiles */
+            return launch_gs<MODE, 0, 2, true, 512>(base, off, delta, nkeys, out, stream, var);
         return d3 ? launch_gs<MODE, 0, 3, true>(base, off, delta, nkeys, out, stream, var)
                   : launch_gs<MODE, 0, 2, true>(base, off, delta, nkeys, out, stream, var);
+    }
     return d3 ? launch_gs<MODE, 0, 3>(base, off, delta, nkeys, out, stream, var)
               : launch_gs<MODE, 0, 2>(base, off, delta, nkeys, out, stream, var);
 }
@@ -2322,7 +2392,7 @@ template <int MODE, int VAR, int P, int DS, int DO, int WPW = 1, int TK = kWrTil
 hipError_t launch_wr_plain(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                            hipStream_t stream)
 {
-    const WrDist none{nullptr, 0u, 0u};
+    const WrDist none{nullptr, 0u, 0u, nullptr};
     return launch_wr<MODE, VAR, P, DS, DO, kDistNone, WPW, TK>(base, off, delta, nkeys, out, stream, none,
                                                                wr_lds_fixed<MODE, kDistNone, P, DS, DO, WPW, TK, VAR>());
 }
@@ -2457,7 +2527,7 @@ hipError_t dist_launch(const uint8_t *base, const uint64_t *off, uint64_t delta,
 {
     constexpr int WPW = 4;
     constexpr size_t kMaxLds = 160u * 1024u;
-    const WrDist wd{d.cont, d.ncont, d.tag};
+    const WrDist wd{d.cont, d.ncont, d.tag, d.lut};
     const size_t fixed = wr_lds_fixed<MODE, kDistKetama, P, DS, DO, WPW>();
     const size_t lds = fixed + 8u * (size_t)d.ncont + (d.kind == 0 ? kBktBytes : 0u);
     if (lds <= kMaxLds) {
@@ -2475,8 +2545,15 @@ hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t 
                              uint32_t *out, hipStream_t stream, const DistArgs &d)
 {
     if constexpr (!uses_crc_table<MODE>()) { /* the crc modes need the workgroup's LDS table slot */
+        if (d.gs) {
+            const WrDist wd{d.cont, d.ncont, d.tag, d.lut};
+            if (d.kind == 0 && d.lut != nullptr)
+                return launch_gs<MODE, 3 << 12, 2, true>(base, off, delta, nkeys, out, stream, d.gs_var, wd);
+            return d.kind == 0 ? launch_gs<MODE, 1 << 12, 2, true>(base, off, delta, nkeys, out, stream, d.gs_var, wd)
+                               : launch_gs<MODE, 2 << 12, 2, true>(base, off, delta, nkeys, out, stream, d.gs_var, wd);
+        }
         if (d.wg) {
-            const WrDist wd{d.cont, d.ncont, d.tag};
+            const WrDist wd{d.cont, d.ncont, d.tag, d.lut};
             return d.kind == 0 ? launch_kernel<MODE, false, 1 << 12>(base, off, delta, nkeys, out, stream, kVarOver, wd)
                                : launch_kernel<MODE, false, 2 << 12>(base, off, delta, nkeys, out, stream, kVarOver, wd);
         }
@@ -2551,9 +2628,13 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
          * one box); one_at_a_time 0.504 (wave-sorted) -> 0.476 at three
          * resident sets (profiles/r03_c2_gsort.jsonl); crc32 / crc32a tie the
          * workgroup x6 and keep it */
-        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarGsort | kVarGsortCs | (2 << 21);
         if (mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A) return kVarWorkgroup | kVarOver;
-        return kVarGsort | kVarGsortCs;
+        if (mode == NC_GPUHASH_CRC16) return kVarGsort | kVarGsortCs; /* its 1 KiB table: four waves */
+        /* 512-key tiles of eight waves, length octiles: fnv1a_64 0.431 ->
+         * 0.409 ms, murmur 0.436 -> 0.403 at three resident sets,
+         * one_at_a_time 0.473 -> 0.465 at six (profiles/r03_c2_gsort.jsonl) */
+        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarGsort | kVarGsortCs | kVarGsort512;
+        return kVarGsort | kVarGsortCs | kVarGsort512 | (2 << 21);
     }
     if (crc || mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarRegStaged | kVarOver;
     return kVarRegStaged;
@@ -2691,14 +2772,43 @@ extern "C" rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint
      * modula 0.56 -> 0.53); modula without a tag on 20+ B keys keeps the wave
      * ring (one continuum read per key, ring 4-11 % ahead on C3).
      * The crc modes always take the ring (their table has the LDS slot).
-     * Variant bit 29 forces the workgroup pipeline, bit 28 the ring (A/B). */
+     * Variant bit 29 forces the workgroup pipeline, bit 28 the ring, bit 30
+     * the grouped pipeline (A/B). */
     const int tuned = load_i(&g_variant);
     bool wg = dist == NC_GPUHASH_DIST_KETAMA || hash_tag != nullptr || !wide;
+    /* keys of varying length under ~22 B (C2) with a hash_tag or modula: the
+     * grouped pipeline, whose waves hash one length quartile each (C2 ketama
+     * with "{}" 1.307 -> 0.897 ms, modula 0.524 -> 0.496; ketama without a
+     * tag ties the workgroup pipeline and keeps it, profiles/r03_sidx.jsonl) */
+    const bool crc = mode == NC_GPUHASH_CRC16 || mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A;
+    bool gs = !crc && shape != nullptr && shape->key_bytes != 0u && shape->key_bytes < 22u * nkeys &&
+              shape->min_len != shape->max_len && (hash_tag != nullptr || dist == NC_GPUHASH_DIST_MODULA);
+    if (tuned & (1 << 30)) gs = true;
+    if (tuned & (3 << 28)) gs = false;
     if (tuned & (1 << 29)) wg = true;
     if (tuned & (1 << 28)) wg = false;
-    nc_tu::DistArgs d{reinterpret_cast<const uint32_t *>(d_continuum), ncontinuum, 0u, dist, wide, wg};
+    nc_tu::DistArgs d{reinterpret_cast<const uint32_t *>(d_continuum), ncontinuum, 0u, dist, wide, wg, gs,
+                      tuned & (3 << 21), nullptr};
     if (hash_tag != nullptr)
         d.tag = (uint32_t)(uint8_t)hash_tag[0] | ((uint32_t)(uint8_t)hash_tag[1] << 8) | (1u << 16);
+    /* A/B only (variant bit 24 with the grouped pipeline): ketama through a
+     * 65536-entry lookup table over the hash's top 16 bits, built on the
+     * stream (~5 us) in stream-ordered scratch: one read per key for most
+     * keys, but of a 256 KiB table that misses L1, where the bucket index's
+     * binary search reads a 10 KiB continuum that stays in it — measured
+     * slower on C2 (0.731 vs 0.687 ms, profiles/r03_sidx.jsonl) */
+    uint32_t *lut = nullptr;
+    if (gs && dist == NC_GPUHASH_DIST_KETAMA && nkeys >= 65536u && (tuned & (1 << 24)) != 0 &&
+        ncontinuum < 0x80000000u && hipMallocAsync((void **)&lut, 65536u * sizeof(uint32_t), st) == hipSuccess) {
+        (void)hipGetLastError();
+        hipLaunchKernelGGL(nc_ketama_lut_kernel, dim3(256), dim3(256), 0, st, d.cont, ncontinuum, lut);
+        if (hipGetLastError() == hipSuccess) {
+            d.lut = lut;
+        } else {
+            (void)hipFreeAsync(lut, st);
+            lut = nullptr;
+        }
+    }
     hipError_t e;
     switch (mode) {
 #define NC_DCASE(M) \
@@ -2717,9 +2827,11 @@ extern "C" rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint
         NC_DCASE(NC_GPUHASH_JENKINS)
 #undef NC_DCASE
     default:
-        return fail(EINVAL);
+        e = hipErrorInvalidValue;
     }
-    if (e != hipSuccess) return fail(e == hipErrorNoDevice ? ENODEV : EIO);
+    if (lut != nullptr) (void)hipFreeAsync(lut, st); /* after the launch that reads it, in stream order */
+    if (e == hipErrorInvalidValue && (mode < 0 || mode >= NC_GPUHASH_NMODES)) return fail(EINVAL);
+    if (e != hipSuccess) return fail_launch(e, "nc_gpuhash_server_idx_device");
     return NC_OK;
 }
 
