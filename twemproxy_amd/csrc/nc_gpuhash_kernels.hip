@@ -34,6 +34,7 @@
 #include "nc_gpuhash.h"
 #include "nc_gpuhash_probe.h"
 #include "nc_hash_algo.h"
+#include "nc_md5_steps.h"
 
 namespace {
 
@@ -1093,7 +1094,8 @@ struct GsLds {
     static constexpr uint32_t kPermBytes = 2u * 2u * TK; /* u16[2][TK]: sorted position -> key index */
     static constexpr uint32_t kResBytes = CS ? 2u * 4u * TK : 0u; /* u32[2][TK]: hashes by key index */
     static constexpr uint32_t kFixed = kNOff * kOffSlot + kPermBytes + 4 * 64 + 4 * 256 + 16 + kResBytes;
-    /* 8 / 7 workgroups of four waves per CU; 4 of eight */
+    /* 8 / 7 workgroups of four waves per CU; 4 of eight (1024-key tiles of
+     * sixteen waves, two per CU, measured 40 % slower) */
     static constexpr uint32_t kBudget = TK == 512 ? 40960 : (D == 2 ? 20480 : 23392);
     static constexpr uint32_t kCap = ((kBudget - kFixed) / D) & ~15u;
     static constexpr uint32_t kOffs = D * kCap;
@@ -1212,6 +1214,56 @@ __device__ __forceinline__ void gs_sort(const uint8_t *slot, uint32_t cnt, uint3
     for (int q = 0; q < KPL; q++) gs_ds_write_b16(perm + 2u * (b[q] + rk[q]), (uint32_t)KPL * lane + (uint32_t)q);
 }
 
+/* md5 of a key in an LDS slab (the grouped pipeline): the direct
+ * pipeline's blocks (padding by byte permutes, the final block's 61 steps,
+ * a data-free tail block when the padding does not fit; src/hashkit/
+ * nc_md5.c:245-321), message words realigned from dword LDS reads. */
+__device__ __forceinline__ uint32_t gs_md5(const uint32_t *slab, uint32_t p, uint32_t len, uint32_t pad_src)
+{
+    using namespace nc_md5s;
+    uint32_t st[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
+    const uint32_t sh = p & 3u;
+    const uint32_t *base = slab + (p >> 2);
+    uint32_t res = 0u;
+    const uint32_t nb = (len + 63u) >> 6; /* blocks holding key bytes */
+    for (uint32_t b = 0; b < nb; b++) {
+        const int32_t rem = (int32_t)len - 64 * (int32_t)b;
+        uint32_t a[17];
+#pragma unroll
+        for (int k = 0; k < 17; k++) a[k] = base[16u * b + (uint32_t)k];
+        md5_u32x4 d[4];
+#pragma unroll
+        for (int k = 0; k < 16; k++) d[k >> 2][k & 3] = __builtin_amdgcn_alignbyte(a[k + 1], a[k], sh);
+        uint32_t w[16];
+        msg_words(d, rem < 64 ? rem : 64, pad_src, w);
+        const bool fin = rem <= 55; /* the bit length fits behind the pad */
+        if (fin) {
+            w[14] = len << 3;
+            w[15] = len >> 29;
+        }
+        uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+        md5_steps(v, w, std::make_integer_sequence<int, 61>{});
+        if (fin) {
+            res = st[0] + v[0]; /* digest bytes 0..3 (nc_md5.c:317-320): state A */
+        } else {
+            md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
+            st[0] += v[0];
+            st[1] += v[1];
+            st[2] += v[2];
+            st[3] += v[3];
+        }
+    }
+    const uint32_t last = len - 64u * (nb ? nb - 1u : 0u); /* key bytes in the last data block */
+    if (len == 0u || last >= 56u) {
+        uint32_t w[16] = {};
+        w[0] = (len & 63u) == 0u ? 0x80u : 0u;
+        w[14] = len << 3;
+        w[15] = len >> 29;
+        res = md5_tail_final_a(st, w);
+    }
+    return res;
+}
+
 template <int MODE, int VAR, int D, bool CS, int TK>
 __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restrict__ keys_base,
                                                         const uint64_t *__restrict__ off, uint64_t delta,
@@ -1288,6 +1340,8 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
         }
     };
 
+    uint32_t pad_src = 0u; /* md5: the padding perms' constant in a VGPR (a uniform selector takes the SGPR slot) */
+    if constexpr (MODE == NC_GPUHASH_MD5) asm volatile("v_mov_b32 %0, %1" : "=v"(pad_src) : "i"(nc_md5s::kPadSrc));
     if (t < 256u) {
         if constexpr (uses_crc_table<MODE>())
             tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
@@ -1376,8 +1430,12 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
             if constexpr ((VAR & 8) != 0) {
                 h = pos ^ len; /* DIAGNOSTIC ONLY: the memory pipeline without hashing */
             } else if (fits(span)) {
-                LdsSrc src{reinterpret_cast<const uint32_t *>(slab_buf(it))};
-                h = wg_value<MODE, VAR>(src, pos, len, tab, tab, dist);
+                if constexpr (MODE == NC_GPUHASH_MD5 && wg_dist<VAR>() == kDistNone) {
+                    h = gs_md5(reinterpret_cast<const uint32_t *>(slab_buf(it)), pos, len, pad_src);
+                } else {
+                    LdsSrc src{reinterpret_cast<const uint32_t *>(slab_buf(it))};
+                    h = wg_value<MODE, VAR>(src, pos, len, tab, tab, dist);
+                }
             } else {
                 GlobalSrc src{reinterpret_cast<const uint32_t *>(keys_base)};
                 h = wg_value<MODE, VAR>(src, S16 + pos, len, tab, tab, dist);
@@ -2629,10 +2687,13 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
          * resident sets (profiles/r03_c2_gsort.jsonl); crc32 / crc32a tie the
          * workgroup x6 and keep it */
         if (mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A) return kVarWorkgroup | kVarOver;
-        if (mode == NC_GPUHASH_CRC16) return kVarGsort | kVarGsortCs; /* its 1 KiB table: four waves */
         /* 512-key tiles of eight waves, length octiles: fnv1a_64 0.431 ->
          * 0.409 ms, murmur 0.436 -> 0.403 at three resident sets,
-         * one_at_a_time 0.473 -> 0.465 at six (profiles/r03_c2_gsort.jsonl) */
+         * one_at_a_time 0.473 -> 0.465 at six; crc16 (its 1 KiB table),
+         * hsieh and jenkins keep 256-key tiles (0.662 vs 0.812, 0.414 vs
+         * 0.417, 0.450 vs 0.459; profiles/r03_c2_gsort.jsonl) */
+        if (mode == NC_GPUHASH_CRC16 || mode == NC_GPUHASH_HSIEH || mode == NC_GPUHASH_JENKINS)
+            return kVarGsort | kVarGsortCs;
         if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarGsort | kVarGsortCs | kVarGsort512;
         return kVarGsort | kVarGsortCs | kVarGsort512 | (2 << 21);
     }

@@ -47,63 +47,6 @@ using namespace nc_md5s;
 
 using namespace nc_direct;
 
-/* ---- message padding by byte permutes ----
- * Word t of a key's last data block, with m = bytes of the key left in the
- * block (1..64): bytes j with 4t + j < m are the key's, byte m is 0x80,
- * the rest are 0. v_perm_b32(d, 0x80000000, sel) picks byte 4+j of d (key
- * byte j), byte 3 of 0x80000000 (the pad) or bytes 0-2 (zero). The selector
- * of word t is clamp(Y0 - t * kStep, 0, kKeep):
- *   kKeep = 0x07060504 (whole word kept), 0 (whole word zero), and for the
- *   word holding byte m (t = m / 4) one of kBoundary[m % 4], which lies
- *   strictly between them; kStep exceeds both gaps, so words before t clamp
- *   to kKeep and words after it to 0. */
-constexpr uint32_t kPadSrc = 0x80000000u;
-constexpr int32_t kKeep = 0x07060504;
-constexpr int32_t kStep = 0x06000000;
-constexpr uint32_t kBoundary0 = 0x02020203u; /* [pad, 0, 0, 0] */
-constexpr uint32_t kBoundary1 = 0x02020304u; /* [key, pad, 0, 0] */
-constexpr uint32_t kBoundary2 = 0x02030504u; /* [key, key, pad, 0] */
-constexpr uint32_t kBoundary3 = 0x03060504u; /* [key, key, key, pad] */
-static_assert(kStep > kKeep - (int32_t)kBoundary0 && kStep > (int32_t)kBoundary3, "selector ordering");
-static_assert(16ll * kStep + (int64_t)kBoundary3 < (1ll << 31), "selector form fits int32");
-
-__device__ __forceinline__ uint32_t pad_word(uint32_t d, int32_t y)
-{
-    const int32_t sel = y < 0 ? 0 : (y > kKeep ? kKeep : y); /* v_med3_i32 */
-    return __builtin_amdgcn_perm(d, kPadSrc, (uint32_t)sel);
-}
-
-/* The 16 message words of a block holding m (1..64) of the key's bytes, the
- * pad byte after them and zeros (no bit length: the caller adds it). When m
- * is the same on every active lane (fixed-length keys) the selectors are
- * wave-uniform and computed on the scalar unit. */
-__device__ __forceinline__ void msg_words(const u32x4 (&d)[4], int32_t m, uint32_t pad_src, uint32_t (&w)[16])
-{
-    const int32_t m0 = __builtin_amdgcn_readfirstlane(m);
-    if (__ballot(m != m0) == 0ull) {
-        const uint32_t r = (uint32_t)m0 & 3u;
-        const uint32_t bnd = r == 0u ? kBoundary0 : (r == 1u ? kBoundary1 : (r == 2u ? kBoundary2 : kBoundary3));
-        const int32_t y0 = (int32_t)bnd + (m0 >> 2) * kStep;
-#pragma unroll
-        for (int t = 0; t < 16; t++) {
-            /* the clamp on the scalar unit (hipcc would use v_med3) and the
-             * selector as the perm's one SGPR operand */
-            uint32_t sel;
-            asm("s_max_i32 %0, %1, 0\n\ts_min_i32 %0, %0, %2" : "=&s"(sel) : "s"(y0 - t * kStep), "s"(kKeep));
-            w[t] = __builtin_amdgcn_perm(d[t >> 2][t & 3], pad_src, sel);
-        }
-    } else {
-        const uint32_t r = (uint32_t)m & 3u;
-        /* kBoundary[r] without branches: two 64-bit selects and a shift */
-        const uint64_t pair = (r & 2u) ? ((uint64_t)kBoundary3 << 32 | kBoundary2)
-                                       : ((uint64_t)kBoundary1 << 32 | kBoundary0);
-        const uint32_t bnd = (uint32_t)(pair >> (32u * (r & 1u)));
-        const int32_t y0 = (int32_t)bnd + (m >> 2) * kStep;
-#pragma unroll
-        for (int t = 0; t < 16; t++) w[t] = pad_word(d[t >> 2][t & 3], y0 - t * kStep);
-    }
-}
-
 /* per-wave LDS queue of keys waiting for their data-free last block */
 constexpr uint32_t kQ = 128;        /* entries per wave (>= 64 + 63) */
 constexpr uint32_t kQWords = 6;     /* A, B, C, D, length, key index */
