@@ -39,7 +39,9 @@ def main():
     shape = cfg["spec"].shape(kb)  # as bench.py: the auto policy's pipeline
     for mode in args.mode.split(","):
         for _ in range(args.iters):
-            if mode == "server_idx":  # bench.py's fused leg: fnv1a_64 + ketama over 8 x 160 points
+            if mode in ("probe_read", "probe_read_nt"):  # FETCH_SIZE calibration: a known byte count
+                t.probe_read_gbs(keys, 1, nt=mode.endswith("_nt"))
+            elif mode == "server_idx":  # bench.py's fused leg: fnv1a_64 + ketama over 8 x 160 points
                 import numpy as np
 
                 rng = np.random.default_rng(9)
