@@ -221,11 +221,15 @@ def test_hash_tag_neighbour_bytes(gpu, oracle, dist_fixture, tag, pipe):
 
 
 def test_ketama_lookup_table(gpu, oracle, dist_fixture):
-    """ketama on the grouped pipeline, with the 65536-entry lookup table
-    (variant bit 24, A/B) and without, and the policy's choice, on batches of
-    64 Ki keys and more: every reference-built pool, a synthetic pool of 300
-    servers (48,000 points, past 2^15) and one whose points crowd a few
-    16-bit ranges, hash tags, against the oracle's server_pool_idx."""
+    """ketama on the grouped pipeline: the continuum staged in LDS with its
+    256-bucket index (the policy's choice up to 4,800 points and 256 servers;
+    256- and 512-key tiles), the same index over the L2 continuum (bit 25), the 65536- and 4096-entry lookup tables in L2
+    (bits 24 / 23, A/B), on batches of 64 Ki keys and more:
+    every reference-built pool, a synthetic pool of 300 servers (48,000
+    points, past 2^15 and past the LDS budget), one whose points crowd a few
+    16-bit ranges, 256 servers (the u8 server bytes' limit) on exactly 4,800
+    points and 4,801 points (just past the LDS limit), hash tags, against the
+    oracle's server_pool_idx."""
     import torch
 
     from twemproxy_amd import _lib as L
@@ -243,13 +247,19 @@ def test_ketama_lookup_table(gpu, oracle, dist_fixture):
     crowd = np.sort(np.concatenate([rng.integers(0, 1 << 18, size=700), rng.integers(0xfffc0000, 1 << 32, size=700),
                                     rng.integers(0, 1 << 32, size=40)]).astype(np.uint64)).astype(np.uint32)
     pools.append((crowd, rng.integers(0, 9, size=crowd.size).astype(np.uint32), 9))
+    for npts in (4800, 4801):
+        v = np.sort(rng.integers(0, 1 << 32, size=npts, dtype=np.uint64)).astype(np.uint32)
+        pools.append((v, rng.integers(0, 256, size=npts).astype(np.uint32), 256))
     try:
         for vals, idx, nserver in pools:
             cd = t.continuum_device(idx, vals)
             for m in (6, 1, 10):
                 for tag in (None, b"{}"):
                     want = oracle.server_idx_batch(m, 0, vals, idx, nserver, tag, keys, off)
-                    for var in ((1 << 30) | (1 << 24), 1 << 30, 0):  # grouped + table, grouped, policy
+                    # grouped + 65536 / 4096 table in L2, grouped + bucket index over the L2 continuum,
+                    # grouped + LDS continuum (256 / 512-key tiles), policy
+                    for var in ((1 << 30) | (1 << 24), (1 << 30) | (1 << 23), (1 << 30) | (1 << 25),
+                                (1 << 30) | (1 << 26), 1 << 30, 0):
                         L.lib().nc_gpuhash_set_tuning(0, 0, var)
                         got = t.server_idx_device(m, "ketama", kd, od, cd, nserver, hash_tag=tag, shape=shape)
                         torch.cuda.synchronize()

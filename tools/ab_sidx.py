@@ -14,7 +14,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 PIPES = {"policy": 0, "ring": 1 << 28, "workgroup": 1 << 29, "grouped": 1 << 30, "grouped3": (1 << 30) | (2 << 21),
-         "grouped1": (1 << 30) | (1 << 21), "grouped_lut": (1 << 30) | (1 << 24)}
+         "grouped1": (1 << 30) | (1 << 21), "grouped_lut16": (1 << 30) | (1 << 24), "grouped_lut12": (1 << 30) | (1 << 23), "grouped512": (1 << 30) | (1 << 26),
+         "workgroup_bkt": (1 << 29) | (1 << 25), "grouped_bkt": (1 << 30) | (1 << 25),
+         "grouped3_bkt": (1 << 30) | (2 << 21) | (1 << 25)}
 GRIDS = {}  # name -> grid cap (--grids: workgroup pipeline at these caps)
 
 

@@ -539,30 +539,38 @@ __device__ __forceinline__ void full_barrier()
     asm volatile("" ::: "memory");
 }
 
-constexpr int kDistNone = -1, kDistKetama = 0, kDistModula = 1, kDistPre = 3, kDistKetamaLut = 4;
+constexpr int kDistNone = -1, kDistKetama = 0, kDistModula = 1, kDistPre = 3, kDistKetamaLut = 4, kDistKetamaLds = 5;
 
 /* server_pool_idx parameters of one launch (ignored for kDistNone) */
 struct WrDist {
     const uint32_t *cont; /* struct continuum {index, value} pairs (src/nc_server.h:64-67) */
     uint32_t ncont;
     uint32_t tag;         /* hash_tag c0 | c1 << 8 | 1 << 16, or 0 for none */
-    const uint32_t *lut;  /* ketama lookup table by the hash's top 16 bits (kDistKetamaLut), or null */
+    const uint32_t *lut;  /* ketama lookup table by the hash's top 32 - lut_shift bits (kDistKetamaLut), or null */
+    uint32_t lut_shift;   /* 20 (4096 entries, L1-resident) or 16 (65536) */
 };
 
-/* ketama_dispatch through a 65536-entry table over the hash's top 16 bits
- * (nc_ketama_lut_kernel): an entry without bit 31 is the server of every
- * hash in its range (no point falls inside the range), else it names the
- * first point >= the range start and the answer is the first point >= h from
- * there (src/hashkit/nc_ketama.c:222-246: the first value >= hash, wrapping
- * to the first point). One L2 read per key for ~98 % of keys of an 8-server
- * pool, instead of a binary search of dependent reads. */
-__device__ __forceinline__ uint32_t ketama_find_lut(const uint32_t *c, const uint32_t *lut, uint32_t n, uint32_t h)
+/* ketama_dispatch through a table over the hash's top bits
+ * (nc_ketama_lut_kernel; 4096 entries = 16 KiB by default, which stays in
+ * the CU's vector L1 beside the continuum): an entry without bit 31 is the
+ * server of every hash in its range (no point falls inside the range), else
+ * it names the first point >= the range start and the answer is the first
+ * point >= h from there (src/hashkit/nc_ketama.c:222-246: the first value >=
+ * hash, wrapping to the first point). For an 8 x 160-point pool ~73 % of keys
+ * resolve with that one read, the rest read ~1.2 {index, value} pairs (one
+ * 8-byte load each) — instead of a binary search of ~4 dependent reads. */
+__device__ __forceinline__ uint32_t ketama_find_lut(const uint32_t *c, const uint32_t *lut, uint32_t shift,
+                                                    uint32_t n, uint32_t h)
 {
-    const uint32_t e = lut[h >> 16];
+    const uint32_t e = lut[h >> shift];
     if ((e >> 31) == 0u) return e;
     uint32_t p = e & 0x7fffffffu;
-    while (p < n && c[2u * p + 1u] < h) p++;
-    return c[2u * (p == n ? 0u : p)];
+    for (;;) {
+        if (p >= n) return c[0]; /* past the last point: wrap */
+        const uint2 iv = reinterpret_cast<const uint2 *>(c)[p];
+        if (iv.y >= h) return iv.x;
+        p++;
+    }
 }
 
 /* hash_tag trimming of server_pool_idx (src/nc_server.c:665-677): the first
@@ -653,6 +661,28 @@ __device__ __forceinline__ uint32_t ketama_find_bkt(const uint32_t *c, const uin
     return c[2u * (lo == n ? 0u : lo)];
 }
 
+/* ketama_dispatch over a continuum staged in LDS (the grouped pipeline):
+ * vals[i] = point i's value, idx[i] = its server (nserver <= 256), bkt the
+ * 256-entry bucket index; every read is an LDS read, where the global form
+ * pays ~4 dependent L2 round trips behind the streaming key traffic */
+__device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const uint8_t *idx, const uint32_t *bkt,
+                                                    uint32_t n, uint32_t h)
+{
+    const uint32_t b = h >> 24;
+    uint32_t lo = bkt[b];
+    uint32_t cnt = (b == 255u ? n : bkt[b + 1u]) - lo;
+    while (cnt > 0u) {
+        const uint32_t half = cnt >> 1;
+        if (vals[lo + half] < h) {
+            lo += half + 1u;
+            cnt -= half + 1u;
+        } else {
+            cnt = half;
+        }
+    }
+    return idx[lo == n ? 0u : lo];
+}
+
 /* lower bound of v over the continuum values (no wrap) */
 __device__ __forceinline__ uint32_t cont_lower_bound(const uint32_t *c, uint32_t n, uint32_t v)
 {
@@ -678,9 +708,10 @@ __device__ __forceinline__ uint32_t cont_lower_bound(const uint32_t *c, uint32_t
 template <int VAR>
 constexpr int wg_dist()
 {
-    return ((VAR >> 12) & 3) == 1   ? kDistKetama
-           : ((VAR >> 12) & 3) == 2 ? kDistModula
-           : ((VAR >> 12) & 3) == 3 ? kDistKetamaLut
+    return ((VAR >> 12) & 7) == 1   ? kDistKetama
+           : ((VAR >> 12) & 7) == 2 ? kDistModula
+           : ((VAR >> 12) & 7) == 3 ? kDistKetamaLut
+           : ((VAR >> 12) & 7) == 4 ? kDistKetamaLds
                                     : kDistNone;
 }
 
@@ -697,10 +728,12 @@ __device__ __forceinline__ uint32_t wg_value(const Src &src, typename Src::pos_t
         if (len != 0u) h = hash_key<MODE, VAR>(src, p, len, tab);
         const uint32_t *c = dist.cont;
         const uint32_t n = dist.ncont;
-        if constexpr (D == kDistModula) {
+        if constexpr (D == kDistKetamaLds) {
+            return h; /* the caller searches its LDS continuum (ketama_find_lds) */
+        } else if constexpr (D == kDistModula) {
             return c[2u * (h % n)]; /* nc_modula.c:153 */
         } else if constexpr (D == kDistKetamaLut) {
-            return ketama_find_lut(c, dist.lut, n, h);
+            return ketama_find_lut(c, dist.lut, dist.lut_shift, n, h);
         } else { /* ketama_dispatch, nc_ketama.c:222-246 */
             const uint32_t b = h >> 24;
             uint32_t lo = bkt[b];
@@ -1214,56 +1247,6 @@ __device__ __forceinline__ void gs_sort(const uint8_t *slot, uint32_t cnt, uint3
     for (int q = 0; q < KPL; q++) gs_ds_write_b16(perm + 2u * (b[q] + rk[q]), (uint32_t)KPL * lane + (uint32_t)q);
 }
 
-/* md5 of a key in an LDS slab (the grouped pipeline): the direct
- * pipeline's blocks (padding by byte permutes, the final block's 61 steps,
- * a data-free tail block when the padding does not fit; src/hashkit/
- * nc_md5.c:245-321), message words realigned from dword LDS reads. */
-__device__ __forceinline__ uint32_t gs_md5(const uint32_t *slab, uint32_t p, uint32_t len, uint32_t pad_src)
-{
-    using namespace nc_md5s;
-    uint32_t st[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
-    const uint32_t sh = p & 3u;
-    const uint32_t *base = slab + (p >> 2);
-    uint32_t res = 0u;
-    const uint32_t nb = (len + 63u) >> 6; /* blocks holding key bytes */
-    for (uint32_t b = 0; b < nb; b++) {
-        const int32_t rem = (int32_t)len - 64 * (int32_t)b;
-        uint32_t a[17];
-#pragma unroll
-        for (int k = 0; k < 17; k++) a[k] = base[16u * b + (uint32_t)k];
-        md5_u32x4 d[4];
-#pragma unroll
-        for (int k = 0; k < 16; k++) d[k >> 2][k & 3] = __builtin_amdgcn_alignbyte(a[k + 1], a[k], sh);
-        uint32_t w[16];
-        msg_words(d, rem < 64 ? rem : 64, pad_src, w);
-        const bool fin = rem <= 55; /* the bit length fits behind the pad */
-        if (fin) {
-            w[14] = len << 3;
-            w[15] = len >> 29;
-        }
-        uint32_t v[4] = {st[0], st[1], st[2], st[3]};
-        md5_steps(v, w, std::make_integer_sequence<int, 61>{});
-        if (fin) {
-            res = st[0] + v[0]; /* digest bytes 0..3 (nc_md5.c:317-320): state A */
-        } else {
-            md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
-            st[0] += v[0];
-            st[1] += v[1];
-            st[2] += v[2];
-            st[3] += v[3];
-        }
-    }
-    const uint32_t last = len - 64u * (nb ? nb - 1u : 0u); /* key bytes in the last data block */
-    if (len == 0u || last >= 56u) {
-        uint32_t w[16] = {};
-        w[0] = (len & 63u) == 0u ? 0x80u : 0u;
-        w[14] = len << 3;
-        w[15] = len >> 29;
-        res = md5_tail_final_a(st, w);
-    }
-    return res;
-}
-
 template <int MODE, int VAR, int D, bool CS, int TK>
 __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restrict__ keys_base,
                                                         const uint64_t *__restrict__ off, uint64_t delta,
@@ -1273,6 +1256,9 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
     using G = GsLds<D, CS, TK>;
     constexpr int kAux = 2; /* nt: read-once streams */
     __shared__ __attribute__((aligned(16))) uint8_t smem[G::kBytes];
+    /* kDistKetamaLds: the continuum's values (u32[ncont]) then servers
+     * (u8[ncont]), in dynamic LDS after smem */
+    extern __shared__ __attribute__((aligned(16))) uint32_t gs_cont[];
     const uint16_t *perm2 = reinterpret_cast<const uint16_t *>(smem + G::kPerm);
     uint32_t *tab = reinterpret_cast<uint32_t *>(smem + G::kTab);
     const uint32_t lds_base = lds_addr(smem);
@@ -1345,7 +1331,15 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
     if (t < 256u) {
         if constexpr (uses_crc_table<MODE>())
             tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
-        if constexpr (wg_dist<VAR>() == kDistKetama) tab[t] = cont_lower_bound(dist.cont, dist.ncont, t << 24);
+        if constexpr (wg_dist<VAR>() == kDistKetama || wg_dist<VAR>() == kDistKetamaLds)
+            tab[t] = cont_lower_bound(dist.cont, dist.ncont, t << 24);
+    }
+    if constexpr (wg_dist<VAR>() == kDistKetamaLds) {
+        uint8_t *ci = reinterpret_cast<uint8_t *>(gs_cont + dist.ncont);
+        for (uint32_t i = t; i < dist.ncont; i += TK) {
+            gs_cont[i] = dist.cont[2u * i + 1u];
+            ci[i] = (uint8_t)dist.cont[2u * i];
+        }
     }
 
     /* prologue: offsets of tiles 0 .. D-1; perm(0); slabs 0 .. D-2 */
@@ -1431,7 +1425,7 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
                 h = pos ^ len; /* DIAGNOSTIC ONLY: the memory pipeline without hashing */
             } else if (fits(span)) {
                 if constexpr (MODE == NC_GPUHASH_MD5 && wg_dist<VAR>() == kDistNone) {
-                    h = gs_md5(reinterpret_cast<const uint32_t *>(slab_buf(it)), pos, len, pad_src);
+                    h = nc_md5s::md5_slab_key(reinterpret_cast<const uint32_t *>(slab_buf(it)), pos, len, pad_src);
                 } else {
                     LdsSrc src{reinterpret_cast<const uint32_t *>(slab_buf(it))};
                     h = wg_value<MODE, VAR>(src, pos, len, tab, tab, dist);
@@ -1441,6 +1435,10 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
                 h = wg_value<MODE, VAR>(src, S16 + pos, len, tab, tab, dist);
                 __builtin_amdgcn_s_waitcnt(0x0070); /* retire the reader's loads before the paths merge */
             }
+            if constexpr (wg_dist<VAR>() == kDistKetamaLds)
+                h = ketama_find_lds(gs_cont, reinterpret_cast<const uint8_t *>(gs_cont + dist.ncont), tab, dist.ncont,
+                                    h);
+
             if constexpr (CS) {
                 gs_ds_write_b32(lds_base + G::kRes + (it & 1u) * 4u * TK + 4u * i, h);
             } else {
@@ -2124,13 +2122,14 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
 }
 
-/* the ketama lookup table (ketama_find_lut): one thread per 16-bit range */
+/* the ketama lookup table (ketama_find_lut): one thread per range of 2^shift
+ * hash values */
 __global__ __launch_bounds__(256) void nc_ketama_lut_kernel(const uint32_t *__restrict__ cont, uint32_t n,
-                                                            uint32_t *__restrict__ lut)
+                                                            uint32_t *__restrict__ lut, uint32_t shift)
 {
     const uint32_t b = blockIdx.x * 256u + threadIdx.x;
-    if (b >= 65536u) return;
-    const uint32_t lo = b << 16, hi = lo | 0xffffu;
+    if (b >= (1u << (32u - shift))) return;
+    const uint32_t lo = b << shift, hi = lo | ((1u << shift) - 1u);
     const uint32_t p = cont_lower_bound(cont, n, lo);
     if (p == n) lut[b] = cont[0];                             /* every hash here wraps to the first point */
     else if (cont[2u * p + 1u] > hi) lut[b] = cont[2u * p];   /* no point inside: one server for the range */
@@ -2190,7 +2189,9 @@ struct DistArgs {
     bool wg;   /* the workgroup pipeline (continuum in L2, bucket index in LDS) instead of the wave ring */
     bool gs;   /* the grouped workgroup pipeline (one length quartile per wave), continuum as for wg */
     int gs_var; /* its launch options (variant bits 21-22: resident sets) */
-    const uint32_t *lut; /* ketama lookup table (ketama_find_lut) for the grouped pipeline, or null */
+    const uint32_t *lut; /* ketama lookup table (ketama_find_lut) for the workgroup pipelines, or null */
+    uint32_t lut_shift;
+    bool lds_cont; /* ketama on the grouped pipeline with the continuum staged in LDS (ketama_find_lds) */
 };
 /* fused hash -> dispatch of mode MODE on the wave ring (offsets 16-byte aligned) */
 template <int MODE>
@@ -2246,6 +2247,7 @@ constexpr int kVarNoFixedLen = 1 << 26; /* md5: no fixed-length specialisation (
 constexpr int kVarGsort = 1 << 25; /* the grouped workgroup pipeline (nc_hash_kernel_gs); options in bits 20-23 */
 constexpr int kVarGsortCs = 1 << 27; /* its hashes stored once per tile, 16 bytes per lane */
 constexpr int kVarGsort512 = 1 << 26; /* with kVarGsortCs: 512-key tiles, eight waves (length octiles) */
+constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline stages in LDS (5 B each) */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2374,15 +2376,19 @@ hipError_t launch_mode(const uint8_t *base, const uint64_t *off, uint64_t delta,
  * workgroups whose tiles ran short hand their slots to new ones. */
 template <int MODE, int VAR, int D, bool CS = false, int TK = 256>
 hipError_t launch_gs(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
-                     hipStream_t stream, int var, const WrDist &dist = WrDist{nullptr, 0u, 0u, nullptr})
+                     hipStream_t stream, int var, const WrDist &dist = WrDist{nullptr, 0u, 0u, nullptr},
+                     size_t dyn_lds = 0)
 {
     void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist) =
         nc_hash_kernel_gs<MODE, VAR, D, CS, TK>;
+    /* occupancy per instantiation and dynamic LDS size (the LDS continuum's) */
     static int per_cu = 0;
-    if (per_cu == 0) {
+    static size_t per_cu_dyn = 0;
+    if (per_cu == 0 || per_cu_dyn != dyn_lds) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, TK, 0) != hipSuccess || b <= 0) b = 4;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, TK, dyn_lds) != hipSuccess || b <= 0) b = 4;
         per_cu = b;
+        per_cu_dyn = dyn_lds;
     }
     static const uint64_t kSets[4] = {6, 1, 3, 8};
     const uint64_t ntiles = (nkeys + TK - 1) / TK;
@@ -2390,7 +2396,8 @@ hipError_t launch_gs(const uint8_t *base, const uint64_t *off, uint64_t delta, u
     uint64_t grid = cap > 0 ? (uint64_t)cap : (uint64_t)num_cus() * (uint64_t)per_cu * kSets[(var >> 21) & 3];
     if (grid > ntiles) grid = ntiles;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(TK), 0, stream, base, off, delta, nkeys, out, ntiles, dist);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(TK), dyn_lds, stream, base, off, delta, nkeys, out, ntiles,
+                       dist);
     return hipGetLastError();
 }
 
@@ -2585,7 +2592,7 @@ hipError_t dist_launch(const uint8_t *base, const uint64_t *off, uint64_t delta,
 {
     constexpr int WPW = 4;
     constexpr size_t kMaxLds = 160u * 1024u;
-    const WrDist wd{d.cont, d.ncont, d.tag, d.lut};
+    const WrDist wd{d.cont, d.ncont, d.tag, d.lut, d.lut_shift};
     const size_t fixed = wr_lds_fixed<MODE, kDistKetama, P, DS, DO, WPW>();
     const size_t lds = fixed + 8u * (size_t)d.ncont + (d.kind == 0 ? kBktBytes : 0u);
     if (lds <= kMaxLds) {
@@ -2604,14 +2611,23 @@ hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t 
 {
     if constexpr (!uses_crc_table<MODE>()) { /* the crc modes need the workgroup's LDS table slot */
         if (d.gs) {
-            const WrDist wd{d.cont, d.ncont, d.tag, d.lut};
+            const WrDist wd{d.cont, d.ncont, d.tag, d.lut, d.lut_shift};
+            if (d.kind == 0 && d.lds_cont) { /* values + u8 servers in dynamic LDS */
+                const size_t vb = (size_t)d.ncont * 4u + (((size_t)d.ncont + 15u) & ~(size_t)15u);
+                if (d.gs_var & kVarGsort512) /* A/B: 512-key tiles (slower: three workgroups per CU) */
+                    return launch_gs<MODE, 4 << 12, 2, true, 512>(base, off, delta, nkeys, out, stream, d.gs_var, wd,
+                                                                   vb);
+                return launch_gs<MODE, 4 << 12, 2, true>(base, off, delta, nkeys, out, stream, d.gs_var, wd, vb);
+            }
             if (d.kind == 0 && d.lut != nullptr)
                 return launch_gs<MODE, 3 << 12, 2, true>(base, off, delta, nkeys, out, stream, d.gs_var, wd);
             return d.kind == 0 ? launch_gs<MODE, 1 << 12, 2, true>(base, off, delta, nkeys, out, stream, d.gs_var, wd)
                                : launch_gs<MODE, 2 << 12, 2, true>(base, off, delta, nkeys, out, stream, d.gs_var, wd);
         }
         if (d.wg) {
-            const WrDist wd{d.cont, d.ncont, d.tag, d.lut};
+            const WrDist wd{d.cont, d.ncont, d.tag, d.lut, d.lut_shift};
+            if (d.kind == 0 && d.lut != nullptr)
+                return launch_kernel<MODE, false, 3 << 12>(base, off, delta, nkeys, out, stream, kVarOver, wd);
             return d.kind == 0 ? launch_kernel<MODE, false, 1 << 12>(base, off, delta, nkeys, out, stream, kVarOver, wd)
                                : launch_kernel<MODE, false, 2 << 12>(base, off, delta, nkeys, out, stream, kVarOver, wd);
         }
@@ -2842,27 +2858,37 @@ extern "C" rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint
      * with "{}" 1.307 -> 0.897 ms, modula 0.524 -> 0.496; ketama without a
      * tag ties the workgroup pipeline and keeps it, profiles/r03_sidx.jsonl) */
     const bool crc = mode == NC_GPUHASH_CRC16 || mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A;
+    /* ketama pools whose continuum fits LDS beside the grouped pipeline's
+     * tiles (values + u8 servers, up to 24 KiB: ~30 servers of 160 points)
+     * take it on C2-like shapes too, the whole search in LDS */
+    const bool lds_cont = dist == NC_GPUHASH_DIST_KETAMA && nserver <= 256u && ncontinuum <= kLdsContMax &&
+                          (tuned & (7 << 23)) == 0;
     bool gs = !crc && shape != nullptr && shape->key_bytes != 0u && shape->key_bytes < 22u * nkeys &&
-              shape->min_len != shape->max_len && (hash_tag != nullptr || dist == NC_GPUHASH_DIST_MODULA);
+              shape->min_len != shape->max_len && (hash_tag != nullptr || dist == NC_GPUHASH_DIST_MODULA || lds_cont);
     if (tuned & (1 << 30)) gs = true;
     if (tuned & (3 << 28)) gs = false;
     if (tuned & (1 << 29)) wg = true;
     if (tuned & (1 << 28)) wg = false;
     nc_tu::DistArgs d{reinterpret_cast<const uint32_t *>(d_continuum), ncontinuum, 0u, dist, wide, wg, gs,
-                      tuned & (3 << 21), nullptr};
+                      tuned & ((3 << 21) | (1 << 26)), nullptr, 20u, gs && lds_cont};
     if (hash_tag != nullptr)
         d.tag = (uint32_t)(uint8_t)hash_tag[0] | ((uint32_t)(uint8_t)hash_tag[1] << 8) | (1u << 16);
-    /* A/B only (variant bit 24 with the grouped pipeline): ketama through a
-     * 65536-entry lookup table over the hash's top 16 bits, built on the
-     * stream (~5 us) in stream-ordered scratch: one read per key for most
-     * keys, but of a 256 KiB table that misses L1, where the bucket index's
-     * binary search reads a 10 KiB continuum that stays in it — measured
-     * slower on C2 (0.731 vs 0.687 ms, profiles/r03_sidx.jsonl) */
+    /* A/B only: ketama on the workgroup pipelines through a lookup table
+     * over the hash's top bits, built on the stream (a few us) in
+     * stream-ordered scratch, so most keys resolve with one read
+     * (ketama_find_lut). Variant bit 24: 65536 entries; bit 23: 4096 (16 KiB).
+     * Both lose to the bucket index's binary search without a hash tag (C2
+     * 0.717 / 0.668-0.688 vs 0.659-0.661 ms, profiles/r03_sidx.jsonl): under
+     * the streaming key traffic a table read is an L2 round trip whatever
+     * its size. Bit 25: the bucket index without the LDS continuum. */
     uint32_t *lut = nullptr;
-    if (gs && dist == NC_GPUHASH_DIST_KETAMA && nkeys >= 65536u && (tuned & (1 << 24)) != 0 &&
-        ncontinuum < 0x80000000u && hipMallocAsync((void **)&lut, 65536u * sizeof(uint32_t), st) == hipSuccess) {
+    if (tuned & (1 << 24)) d.lut_shift = 16u;
+    const size_t lut_n = (size_t)1 << (32u - d.lut_shift);
+    if ((gs || wg) && dist == NC_GPUHASH_DIST_KETAMA && nkeys >= 65536u && (tuned & (3 << 23)) != 0 && !crc &&
+        ncontinuum < 0x80000000u && hipMallocAsync((void **)&lut, lut_n * sizeof(uint32_t), st) == hipSuccess) {
         (void)hipGetLastError();
-        hipLaunchKernelGGL(nc_ketama_lut_kernel, dim3(256), dim3(256), 0, st, d.cont, ncontinuum, lut);
+        hipLaunchKernelGGL(nc_ketama_lut_kernel, dim3((unsigned)((lut_n + 255u) / 256u)), dim3(256), 0, st, d.cont,
+                           ncontinuum, lut, d.lut_shift);
         if (hipGetLastError() == hipSuccess) {
             d.lut = lut;
         } else {

@@ -206,6 +206,67 @@ __device__ __forceinline__ void msg_words(const md5_u32x4 (&d)[4], int32_t m, ui
     }
 }
 
+/* The message words y0 selector of a key of m (0..64) bytes in its last
+ * data block, per lane: kBoundary[m % 4] + (m / 4) * kStep, no branches */
+__device__ __forceinline__ int32_t pad_y0(uint32_t m)
+{
+    const uint32_t r = m & 3u;
+    const uint64_t pair = (r & 2u) ? ((uint64_t)kBoundary3 << 32 | kBoundary2) : ((uint64_t)kBoundary1 << 32 | kBoundary0);
+    const uint32_t bnd = (uint32_t)(pair >> (32u * (r & 1u)));
+    return (int32_t)bnd + (int32_t)(m >> 2) * kStep;
+}
+
+/* md5 of a key of len bytes at byte p of a dword-readable slab (LDS, or a
+ * 16-byte aligned global buffer): the direct pipeline's blocks (padding by
+ * byte permutes, the final block's 61 steps, a data-free tail block when the
+ * padding does not fit; src/hashkit/nc_md5.c:245-321), message words
+ * realigned from dword reads. Reads up to 68 bytes past each block's start. */
+template <class Words>
+__device__ __forceinline__ uint32_t md5_slab_key(const Words &slab, uint32_t p, uint32_t len, uint32_t pad_src)
+{
+    uint32_t st[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
+    const uint32_t sh = p & 3u;
+    const uint32_t w0 = p >> 2;
+    uint32_t res = 0u;
+    const uint32_t nb = (len + 63u) >> 6; /* blocks holding key bytes */
+    for (uint32_t b = 0; b < nb; b++) {
+        const int32_t rem = (int32_t)len - 64 * (int32_t)b;
+        uint32_t a[17];
+#pragma unroll
+        for (int k = 0; k < 17; k++) a[k] = slab[w0 + 16u * b + (uint32_t)k];
+        md5_u32x4 d[4];
+#pragma unroll
+        for (int k = 0; k < 16; k++) d[k >> 2][k & 3] = __builtin_amdgcn_alignbyte(a[k + 1], a[k], sh);
+        uint32_t w[16];
+        msg_words(d, rem < 64 ? rem : 64, pad_src, w);
+        const bool fin = rem <= 55; /* the bit length fits behind the pad */
+        if (fin) {
+            w[14] = len << 3;
+            w[15] = len >> 29;
+        }
+        uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+        md5_steps(v, w, std::make_integer_sequence<int, 61>{});
+        if (fin) {
+            res = st[0] + v[0]; /* digest bytes 0..3 (nc_md5.c:317-320): state A */
+        } else {
+            md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
+            st[0] += v[0];
+            st[1] += v[1];
+            st[2] += v[2];
+            st[3] += v[3];
+        }
+    }
+    const uint32_t last = len - 64u * (nb ? nb - 1u : 0u); /* key bytes in the last data block */
+    if (len == 0u || last >= 56u) {
+        uint32_t w[16] = {};
+        w[0] = (len & 63u) == 0u ? 0x80u : 0u;
+        w[14] = len << 3;
+        w[15] = len >> 29;
+        res = md5_tail_final_a(st, w);
+    }
+    return res;
+}
+
 } // namespace nc_md5s
 
 #endif
