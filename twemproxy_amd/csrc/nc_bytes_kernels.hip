@@ -51,24 +51,17 @@ __device__ __forceinline__ uint32_t final_state(uint32_t h)
     return h;
 }
 
-/* ---- crc tables: slicing-by-4 (nc_crc_slice.h), replicated over R bank
- * groups: R = 8 (32 KiB) beside the line image, NC_CRC_COPIES_REG on the
- * register path ---- */
-#ifndef NC_CRC_COPIES_REG
-#define NC_CRC_COPIES_REG 8
-#endif
-template <bool LDS>
-constexpr uint32_t copies()
-{
-    return LDS ? 8u : (uint32_t)NC_CRC_COPIES_REG;
-}
+/* ---- crc tables: slicing-by-4 (nc_crc_slice.h), replicated over 8 bank
+ * groups (R = 8, 32 KiB) ---- */
+constexpr uint32_t kCopies = 8;
+constexpr uint32_t kTabWords = nc_slice::table_words<kCopies>();
 
 /* byte j (0..3) of word w into state h (the crcs through T0) */
-template <int MODE, uint32_t R>
+template <int MODE>
 __device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t w, int j, const uint32_t *tab, uint32_t lane4)
 {
     const uint32_t b = (w >> (8 * j)) & 0xffu;
-    if constexpr (has_table<MODE>()) return nc_slice::byte<MODE, R>(h, b, tab, lane4);
+    if constexpr (has_table<MODE>()) return nc_slice::byte<MODE, kCopies>(h, b, tab, lane4);
     else if constexpr (MODE == NC_GPUHASH_FNV1A_64) return nc_fnv1a_64_step(h, b);
     else if constexpr (MODE == NC_GPUHASH_FNV1_64) return nc_fnv1_64_step(h, b);
     else if constexpr (MODE == NC_GPUHASH_FNV1_32) return nc_fnv1_32_step(h, b);
@@ -77,30 +70,30 @@ __device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t w, int j, con
 }
 
 /* the 4 bytes of word w */
-template <int MODE, uint32_t R>
+template <int MODE>
 __device__ __forceinline__ uint32_t word_step(uint32_t h, uint32_t w, const uint32_t *tab, uint32_t lc4)
 {
     if constexpr (has_table<MODE>()) {
-        return nc_slice::word<MODE, R>(h, w, tab, lc4);
+        return nc_slice::word<MODE, kCopies>(h, w, tab, lc4);
     } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++) h = byte_step<MODE, R>(h, w, j, tab, lc4);
+        for (int j = 0; j < 4; j++) h = byte_step<MODE>(h, w, j, tab, lc4);
         return h;
     }
 }
 
 /* the first nb (1..4, per lane) bytes of word w, one at a time */
-template <int MODE, uint32_t R>
+template <int MODE>
 __device__ __forceinline__ uint32_t bytes_step(uint32_t h, uint32_t w, int32_t nb, const uint32_t *tab, uint32_t lc4)
 {
 #pragma unroll
     for (int j = 0; j < 4; j++)
-        if (j < nb) h = byte_step<MODE, R>(h, w, j, tab, lc4);
+        if (j < nb) h = byte_step<MODE>(h, w, j, tab, lc4);
     return h;
 }
 
 /* nb (per lane, may exceed 64) key bytes of one block in d */
-template <int MODE, uint32_t R>
+template <int MODE>
 __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], int32_t nb, const uint32_t *tab,
                                                uint32_t lane4)
 {
@@ -111,8 +104,8 @@ __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], 
         /* crc16 keeps its key's last 2+ bytes for the byte steps, which
          * rebuild the state's history bits (nc_crc_slice.h word) */
         constexpr int32_t kWhole = nc_slice::whole<MODE>();
-        if (kb >= kWhole) h = word_step<MODE, R>(h, w, tab, lane4);
-        else if (kb > 0) h = bytes_step<MODE, R>(h, w, kb, tab, lane4);
+        if (kb >= kWhole) h = word_step<MODE>(h, w, tab, lane4);
+        else if (kb > 0) h = bytes_step<MODE>(h, w, kb, tab, lane4);
     }
     return h;
 }
@@ -134,16 +127,15 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
     /* a round consumes RB bytes of every key: one 64-byte block from
      * registers, or (LDS) one 128-byte line from the image */
     constexpr uint32_t RB = LDS ? 128u : 64u;
-    constexpr uint32_t R = copies<LDS>();
-    __shared__ uint32_t tab[has_table<MODE>() ? nc_slice::table_words<R>() : 1];
+    __shared__ uint32_t tab[has_table<MODE>() ? kTabWords : 1];
     __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kLineImage : 16];
     if constexpr (has_table<MODE>()) {
-        nc_slice::fill<MODE, R>(tab, threadIdx.x, 1024u);
+        nc_slice::fill<MODE, kCopies>(tab, threadIdx.x, 1024u);
         __syncthreads();
     }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane4 = nc_slice::copy_of<R>(lane); /* this lane's table copy */
+    const uint32_t lane4 = nc_slice::copy_of<kCopies>(lane); /* this lane's table copy */
     const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
     uint64_t tile = 0; /* local tile index */
     const uint64_t tlast = tiles.n;
@@ -178,9 +170,9 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
 
         const int32_t rem = (int32_t)cur_t.len - (int32_t)RB * (int32_t)b;
         if (cur_t.valid && (rem > 0 || (b == 0u && cur_t.len == 0u))) {
-            h = block_step<MODE, R>(h, cur, rem, tab, lane4);
+            h = block_step<MODE>(h, cur, rem, tab, lane4);
             if constexpr (LDS) {
-                if (rem > 64) h = block_step<MODE, R>(h, nxt, rem - 64, tab, lane4);
+                if (rem > 64) h = block_step<MODE>(h, nxt, rem - 64, tab, lane4);
             }
             if (rem <= (int32_t)RB) {
                 const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);

@@ -1347,7 +1347,7 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
     for (uint32_t j = 0; j < (uint32_t)D; j++) gs_issue_offs<kAux, TK>(off, tile_at(j), nkeys, offs_slot(j), t);
     full_barrier();
     uint32_t cnt = gs_tile_count<TK>(tile, nkeys);
-    if (wave == 0u && (VAR & 16) == 0) gs_sort<TK>(offs_slot(0), cnt, lds_base + G::kHist, lds_base + G::kPerm, lane);
+    if (wave == 0u) gs_sort<TK>(offs_slot(0), cnt, lds_base + G::kHist, lds_base + G::kPerm, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     uint64_t S16, span;
     bounds(offs_slot(0), S16, span);
@@ -1405,8 +1405,7 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
         asm volatile("" ::: "memory");
         /* wave 0 sorts tile t+1 with its DMAs already out (every LDS access
          * of the sort is inline asm, which hipcc does not hold behind them) */
-        /* VAR bit 4 (A/B): no length grouping, wave w hashes keys 64w.. */
-        if (more && wave == 0u && (VAR & 16) == 0)
+        if (more && wave == 0u)
             gs_sort<TK>(offs_slot(it + 1u), cnt1, lds_base + G::kHist, lds_base + G::kPerm + ((it + 1u) & 1u) * 2u * TK,
                         lane);
         asm volatile("" ::: "memory");
@@ -1415,7 +1414,7 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
         const uint8_t *slot = offs_slot(it);
         const uint32_t j = 64u * wave + lane;
         if (j < cnt) {
-            const uint32_t i = (VAR & 16) ? j : perm2[(it & 1u) * TK + j];
+            const uint32_t i = perm2[(it & 1u) * TK + j];
             const uint32_t s = gs_lo(slot, i);
             /* the DMA clamps at nkeys, so [cnt] holds the end of a partial
              * tile's last key; a full tile's ends at the end bound, [TK] */
@@ -2248,7 +2247,6 @@ constexpr int kVarNoFixedLen = 1 << 26; /* md5: no fixed-length specialisation (
 constexpr int kVarGsort = 1 << 25; /* the grouped workgroup pipeline (nc_hash_kernel_gs); options in bits 20-23 */
 constexpr int kVarGsortCs = 1 << 27; /* its hashes stored once per tile, 16 bytes per lane */
 constexpr int kVarGsort512 = 1 << 26; /* with kVarGsortCs: 512-key tiles, eight waves (length octiles) */
-constexpr int kVarGsortNoSort = 1 << 28; /* A/B: the grouped pipeline's tiles without the length sort */
 constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline stages in LDS (5 B each) */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
@@ -2418,8 +2416,6 @@ hipError_t launch_gs_mode(const uint8_t *base, const uint64_t *off, uint64_t del
         }
     }
     if (var & kVarGsortCs) { /* the previous tile's hashes as one coalesced store */
-        if ((var & kVarGsortNoSort) != 0 && (var & kVarGsort512) != 0) /* A/B: 512-key tiles without the sort */
-            return launch_gs<MODE, 16, 2, true, 512>(base, off, delta, nkeys, out, stream, var);
         if (var & kVarGsort512) /* 512-key tiles, eight waves, length octiles */
             return launch_gs<MODE, 0, 2, true, 512>(base, off, delta, nkeys, out, stream, var);
         return d3 ? launch_gs<MODE, 0, 3, true>(base, off, delta, nkeys, out, stream, var)
