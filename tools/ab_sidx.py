@@ -29,7 +29,12 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--grids", default="", help="comma-separated grid caps for extra workgroup entries")
+    ap.add_argument("--pipes", default="", help="comma-separated subset of the pipeline names")
+    ap.add_argument("--lib", default="", help="another build of libnc_gpuhash.so (same-box A/B of builds)")
     args = ap.parse_args()
+    if args.pipes:
+        for k in [k for k in PIPES if k not in args.pipes.split(",")]:
+            del PIPES[k]
     for g in filter(None, args.grids.split(",")):
         PIPES[f"workgroup_g{g}"] = 1 << 29
         GRIDS[f"workgroup_g{g}"] = int(g)
@@ -37,8 +42,11 @@ def main():
     import numpy as np
     import torch
 
-    import twemproxy_amd as t
     from twemproxy_amd import _lib as L
+
+    if args.lib:
+        L.LIB_PATH = os.path.abspath(args.lib)
+    import twemproxy_amd as t
 
     rng = np.random.default_rng(9)
     cvals = np.sort(rng.integers(0, 1 << 32, size=8 * 160, dtype=np.uint64)).astype(np.uint32)
@@ -85,7 +93,7 @@ def main():
                         res[name] = (round(statistics.median(ms), 4), chk)
                     L.lib().nc_gpuhash_set_tuning(0, 0, 0)
                     alg = kb + 12.0 * n
-                    print(json.dumps({"config": cfg, "mode": mode, "dist": dist, "tag": tag,
+                    print(json.dumps({"lib": os.path.basename(L.LIB_PATH), "config": cfg, "mode": mode, "dist": dist, "tag": tag,
                                       "ms": {k: v[0] for k, v in res.items()},
                                       "frac": {k: round(alg / v[0] / 1e6 / 8000.0, 4) for k, v in res.items()},
                                       "check": {k: v[1] for k, v in res.items()}}), flush=True)
