@@ -143,7 +143,7 @@ def test_auto_policy_choices():
     WG, RS, RING5, RING4 = 1 << 16, 32, 128 | (3 << 8), 128
     SORTED, OVER = 1 << 17, 1 << 18
     DIRECT, DIRECT_LDS, IL32 = 1 << 19, 4 << 20, (8 | 2) << 20
-    GSORT, CS, TK512 = 1 << 25, 1 << 27, 1 << 26
+    GSORT, CS, TK512, ISSUE = 1 << 25, 1 << 27, 1 << 26, 1 << 28
     n = 1 << 26
     assert t.pick_variant("fnv1a_64", n) == RS
     assert t.pick_variant("md5", n) == DIRECT  # unknown shape
@@ -153,8 +153,8 @@ def test_auto_policy_choices():
     for name in ("crc16", "hsieh", "jenkins"):
         assert t.pick_variant(name, n, (19 * n, 8, 64)) == GSORT | CS, name
     assert t.pick_variant("crc32", n, (19 * n, 8, 64)) == WG | OVER
-    assert t.pick_variant("one_at_a_time", n, (19 * n, 8, 64)) == GSORT | CS | TK512
-    assert t.pick_variant("one_at_a_time", n, (21 * n, 8, 64)) == GSORT | CS | TK512
+    assert t.pick_variant("one_at_a_time", n, (19 * n, 8, 64)) == GSORT | CS | TK512 | ISSUE
+    assert t.pick_variant("one_at_a_time", n, (21 * n, 8, 64)) == GSORT | CS | TK512 | ISSUE
     assert t.pick_variant("md5", n, (19 * n, 8, 64)) == DIRECT
     # uniform 8-64 B (mean 36)
     assert t.pick_variant("fnv1a_64", n, (36 * n, 8, 64)) == RS

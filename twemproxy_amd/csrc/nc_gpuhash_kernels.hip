@@ -1384,9 +1384,12 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
     };
     for (uint32_t it = 0;; it++) {
         top_barrier(); /* slab(it), offsets(it+1 .. it+D-1), perm(it) in LDS; reads of reused buffers done */
-        if constexpr (CS) {
+        /* VAR bit 6 (D = 2): the DMAs go out first — no second read of the
+         * same bounds, the previous tile's coalesced store after them */
+        constexpr bool kIssueFirst = (VAR & 64) != 0 && D == 2 && CS;
+        if constexpr (CS && !kIssueFirst) {
             if (pend_tile != ~0ull) store_tile();
-        } else {
+        } else if constexpr (!CS) {
             if (pend_idx != ~0ull) __builtin_nontemporal_store(pend_h, out + pend_idx);
             pend_idx = ~0ull;
         }
@@ -1396,13 +1399,22 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
         const uint32_t cnt1 = more ? gs_tile_count<TK>(t1, nkeys) : 0u;
         /* every LDS read of the offsets slots comes before this iteration's
          * DMAs */
-        uint64_t S16n = 0, spann = 0, sn, pn;
+        uint64_t S16n = 0, spann = 0, sn = 0, pn = 0;
         if (more) bounds(offs_slot(it + 1u), S16n, spann);
-        bounds(offs_slot(it + (uint32_t)D - 1u), sn, pn); /* slab(t + D - 1) */
+        if constexpr (kIssueFirst) { /* slab(t + 1): the bounds just read */
+            sn = S16n;
+            pn = spann;
+        } else {
+            bounds(offs_slot(it + (uint32_t)D - 1u), sn, pn); /* slab(t + D - 1) */
+        }
         const bool dn = tile + (uint64_t)(D - 1) * stride < ntiles && fits(pn);
         gs_issue_offs<kAux, TK>(off, tile_at(D), nkeys, offs_slot(it + (uint32_t)D), t);
         slab_dma(dn, sn, pn, slab_buf(it + (uint32_t)D - 1u));
         asm volatile("" ::: "memory");
+        if constexpr (kIssueFirst) {
+            if (pend_tile != ~0ull) store_tile();
+            asm volatile("" ::: "memory");
+        }
         /* wave 0 sorts tile t+1 with its DMAs already out (every LDS access
          * of the sort is inline asm, which hipcc does not hold behind them) */
         if (more && wave == 0u)
@@ -2247,6 +2259,7 @@ constexpr int kVarNoFixedLen = 1 << 26; /* md5: no fixed-length specialisation (
 constexpr int kVarGsort = 1 << 25; /* the grouped workgroup pipeline (nc_hash_kernel_gs); options in bits 20-23 */
 constexpr int kVarGsortCs = 1 << 27; /* its hashes stored once per tile, 16 bytes per lane */
 constexpr int kVarGsort512 = 1 << 26; /* with kVarGsortCs: 512-key tiles, eight waves (length octiles) */
+constexpr int kVarGsortIssue = 1 << 28; /* A/B: the grouped tile's DMAs issued before the previous tile's store */
 constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline stages in LDS (5 B each) */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
@@ -2416,6 +2429,8 @@ hipError_t launch_gs_mode(const uint8_t *base, const uint64_t *off, uint64_t del
         }
     }
     if (var & kVarGsortCs) { /* the previous tile's hashes as one coalesced store */
+        if ((var & kVarGsortIssue) != 0 && (var & kVarGsort512) != 0) /* A/B: DMAs before the store */
+            return launch_gs<MODE, 64, 2, true, 512>(base, off, delta, nkeys, out, stream, var);
         if (var & kVarGsort512) /* 512-key tiles, eight waves, length octiles */
             return launch_gs<MODE, 0, 2, true, 512>(base, off, delta, nkeys, out, stream, var);
         return d3 ? launch_gs<MODE, 0, 3, true>(base, off, delta, nkeys, out, stream, var)
@@ -2710,7 +2725,10 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
          * 0.417, 0.450 vs 0.459; profiles/r03_c2_gsort.jsonl) */
         if (mode == NC_GPUHASH_CRC16 || mode == NC_GPUHASH_HSIEH || mode == NC_GPUHASH_JENKINS)
             return kVarGsort | kVarGsortCs;
-        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarGsort | kVarGsortCs | kVarGsort512;
+        /* one_at_a_time (the most VALU per byte) issues a tile's DMAs before
+         * the previous tile's store: 0.464 -> 0.453 ms; fnv x4 / murmur lose
+         * ~1 % that way (profiles/r03_c2_gs_ab.jsonl) */
+        if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarGsort | kVarGsortCs | kVarGsort512 | kVarGsortIssue;
         return kVarGsort | kVarGsortCs | kVarGsort512 | (2 << 21);
     }
     if (crc || mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarRegStaged | kVarOver;
