@@ -186,10 +186,14 @@ def md5_ceiling():
 
 def read_ceiling(t, rf, buf):
     """Same-run STREAM-style read ceiling over the key buffer:
-    the achievable HBM read rate on this box, after the timed region."""
+    the achievable HBM read rate on this box, after the timed region, with
+    default and with non-temporal loads (the hash kernels stream with nt)."""
     probe = t.probe_read_gbs(buf, 20)
     rf["read_ceiling_gbs"] = round(probe, 1)
     rf["frac_of_read_ceiling"] = round(rf["achieved"] / probe, 4)
+    probe_nt = t.probe_read_gbs(buf, 20, nt=True)
+    rf["read_ceiling_nt_gbs"] = round(probe_nt, 1)
+    rf["frac_of_read_ceiling_nt"] = round(rf["achieved"] / probe_nt, 4)
 
 
 SHARD_DIGESTS = os.path.join(HERE, "tests", "golden", "shard_digests.json")
