@@ -2265,6 +2265,21 @@ constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline sta
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
 
+/* Occupancy of one kernel instantiation at one dynamic LDS size, cached as
+ * ONE word (lds << 32 | blocks per CU) so threads launching with different
+ * LDS sizes (different continuum sizes) never read a torn pair; a miss just
+ * asks HIP again. */
+template <class K>
+int cached_occupancy(uint64_t *cache, K kern, int block, size_t lds, int dflt)
+{
+    const uint64_t v = __atomic_load_n(cache, __ATOMIC_RELAXED);
+    if ((uint32_t)v != 0u && (v >> 32) == (uint64_t)lds) return (int)(uint32_t)v;
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, block, lds) != hipSuccess || b <= 0) b = dflt;
+    __atomic_store_n(cache, ((uint64_t)lds << 32) | (uint32_t)b, __ATOMIC_RELAXED);
+    return b;
+}
+
 int grid_cap()
 {
     int v = load_i(&g_grid_cap);
@@ -2311,12 +2326,8 @@ hipError_t launch_kernel(const uint8_t *base, const uint64_t *off, uint64_t delt
     void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist);
     if constexpr ((VAR & 32) != 0) kern = nc_hash_kernel_rs<MODE, SORT, VAR>;
     else kern = nc_hash_kernel<MODE, SORT, VAR>;
-    static int per_cu = 0;
-    if (per_cu == 0) {
-        int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, kBlock, 0) != hipSuccess || b <= 0) b = 4;
-        per_cu = b;
-    }
+    static uint64_t occ = 0;
+    const int per_cu = cached_occupancy(&occ, kern, kBlock, 0, 4);
     const uint64_t ntiles = (nkeys + kTile - 1) / kTile;
     const int cap = grid_cap();
     /* kVarOver: three resident sets of workgroups instead of one. The grid
@@ -2395,14 +2406,8 @@ hipError_t launch_gs(const uint8_t *base, const uint64_t *off, uint64_t delta, u
     void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist) =
         nc_hash_kernel_gs<MODE, VAR, D, CS, TK>;
     /* occupancy per instantiation and dynamic LDS size (the LDS continuum's) */
-    static int per_cu = 0;
-    static size_t per_cu_dyn = 0;
-    if (per_cu == 0 || per_cu_dyn != dyn_lds) {
-        int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, TK, dyn_lds) != hipSuccess || b <= 0) b = 4;
-        per_cu = b;
-        per_cu_dyn = dyn_lds;
-    }
+    static uint64_t occ = 0;
+    const int per_cu = cached_occupancy(&occ, kern, TK, dyn_lds, 4);
     static const uint64_t kSets[4] = {6, 1, 3, 8};
     const uint64_t ntiles = (nkeys + TK - 1) / TK;
     const int cap = grid_cap();
@@ -2448,15 +2453,9 @@ hipError_t launch_wr(const uint8_t *base, const uint64_t *off, uint64_t delta, u
 {
     void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist) =
         nc_hash_kernel_wr<MODE, VAR, P, DS, DO, DIST, WPW, TK>;
-    static size_t cached_lds = 0;
-    static int per_cu = 0;
-    if (per_cu == 0 || cached_lds != lds) {
-        if (lds > 65536u) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * WPW, lds) != hipSuccess || b <= 0) b = 1;
-        per_cu = b;
-        cached_lds = lds;
-    }
+    if (lds > 65536u) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    static uint64_t occ = 0;
+    const int per_cu = cached_occupancy(&occ, kern, 64 * WPW, lds, 1);
     const uint64_t ntiles = (nkeys + TK - 1) / TK;
     const uint64_t max_grid = (ntiles + WPW - 1) / WPW;
     const int cap = grid_cap();
