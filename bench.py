@@ -187,13 +187,19 @@ def md5_ceiling():
 def read_ceiling(t, rf, buf):
     """Same-run STREAM-style read ceiling over the key buffer:
     the achievable HBM read rate on this box, after the timed region, with
-    default and with non-temporal loads (the hash kernels stream with nt)."""
+    default and with non-temporal loads (the hash kernels stream with nt),
+    and the read+write mix of a hash kernel (profiles/r03_cache_policy_ab.md)."""
     probe = t.probe_read_gbs(buf, 20)
     rf["read_ceiling_gbs"] = round(probe, 1)
     rf["frac_of_read_ceiling"] = round(rf["achieved"] / probe, 4)
     probe_nt = t.probe_read_gbs(buf, 20, nt=True)
     rf["read_ceiling_nt_gbs"] = round(probe_nt, 1)
     rf["frac_of_read_ceiling_nt"] = round(rf["achieved"] / probe_nt, 4)
+    # a hash kernel also writes (4 B per key: ~12 % of C2's bytes); the mix
+    # probe is the nt read plus one nt 16-B store per 128 B read
+    mix = t.probe_mix_gbs(buf, 20)
+    rf["mix_ceiling_gbs"] = round(mix, 1)
+    rf["frac_of_mix_ceiling"] = round(rf["achieved"] / mix, 4)
 
 
 SHARD_DIGESTS = os.path.join(HERE, "tests", "golden", "shard_digests.json")

@@ -28,6 +28,13 @@ rstatus_t nc_gpuhash_probe_read(const void *d_buf, uint64_t bytes, uint32_t *d_s
  * under the cache policy of launch variant bit 6. */
 rstatus_t nc_gpuhash_probe_read_nt(const void *d_buf, uint64_t bytes, uint32_t *d_sink, void *stream, int iters,
                                    float *avg_ms);
+/* The read/write mix of a hash kernel: the read of `bytes` plus one 16-byte
+ * store per 128 bytes read (12.5 % of the bytes moved are writes; C2
+ * fnv1a_64's are 12 %) into d_wout, which must hold
+ * ceil(bytes / 32768) * 4096 bytes. policy: bit 0 the loads, bit 1 the stores
+ * with the default cache policy instead of non-temporal (EINVAL otherwise). */
+rstatus_t nc_gpuhash_probe_mix(const void *d_buf, uint64_t bytes, void *d_wout, uint64_t wout_bytes,
+                               uint32_t *d_sink, void *stream, int policy, int iters, float *avg_ms);
 
 /* The launch variant the auto policy picks for this mode and shape (the
  * variant bits of nc_gpuhash_set_tuning; bit 16 = the plain workgroup

@@ -180,3 +180,27 @@ def test_pinned_pipe_registered_numpy_and_limits(gpu, oracle):
     finally:
         for a in (keys_np, off_np, out):
             t.host_unregister(a.ctypes.data)
+
+
+def test_probe_mix_contract():
+    """nc_gpuhash_probe_mix: a positive rate for every policy, EINVAL for an
+    output buffer below ceil(bytes / 32768) * 4096 or an unknown policy."""
+    import ctypes
+
+    import torch
+
+    import twemproxy_amd as t
+    from twemproxy_amd import _lib as L
+
+    buf = torch.randint(0, 256, (1 << 24,), dtype=torch.uint8, device="cuda")
+    for pol in range(4):
+        assert t.probe_mix_gbs(buf, 2, policy=pol) > 0
+    need = -(-buf.numel() // 32768) * 4096
+    wout = torch.empty(need, dtype=torch.uint8, device="cuda")
+    sink = torch.zeros(65536, dtype=torch.int32, device="cuda")
+    ms = ctypes.c_float(0.0)
+    f = L.lib().nc_gpuhash_probe_mix
+    assert f(buf.data_ptr(), buf.numel(), wout.data_ptr(), need - 16, sink.data_ptr(), None, 0, 1,
+             ctypes.byref(ms)) != 0
+    assert f(buf.data_ptr(), buf.numel(), wout.data_ptr(), need, sink.data_ptr(), None, 4, 1, ctypes.byref(ms)) != 0
+    assert f(buf.data_ptr(), buf.numel(), wout.data_ptr(), need, sink.data_ptr(), None, 0, 1, ctypes.byref(ms)) == 0

@@ -173,6 +173,11 @@ SIGNATURES = {
         [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
          ctypes.POINTER(ctypes.c_float)],
     ),
+    "nc_gpuhash_probe_mix": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)],
+    ),
     # synthetic generator
     "nc_synth_lengths_host": (
         ctypes.c_int, [ctypes.POINTER(NcSynthSpec), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]

@@ -115,14 +115,16 @@ struct Walker {
      * that every round issues the same loads (keys past nkeys read as 0).
      * (Measured: taking a key's end from the next lane by DPP, or the tile
      * base by vector load + v_readlane, costs md5 1.5 % each and gains the
-     * crcs nothing.) */
+     * crcs nothing.) AUX: the loads' cache policy — streaming for the byte
+     * kernels, the default for md5 (profiles/r03_cache_policy_ab.md). */
+    template <int AUX = kAuxNt>
     __device__ __forceinline__ Offs load_off(uint64_t tl) const
     {
         const uint64_t k0 = key0(tl < tlast ? tl : tlast - 1u);
         const rsrc_t r = make_rsrc(off + k0, (nkeys + 1u - k0) * 8u);
         Offs o;
-        o.s = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u), 0, kAuxNt);
-        o.e = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u + 8u), 0, kAuxNt);
+        o.s = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u), 0, AUX);
+        o.e = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u + 8u), 0, AUX);
         o.s0 = off[k0];
         return o;
     }

@@ -121,9 +121,11 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
     };
 
     /* prologue: offsets of the first tile (waited), of the second (in
-     * flight), block 0 of the first tile (in flight) */
-    TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
-    Offs no = wk.load_off(tile + 1u);
+     * flight), block 0 of the first tile (in flight). The offsets take the
+     * default cache policy here (the byte kernels' nt is 2 % slower for md5:
+     * C2 0.787 -> 0.772 ms in an A/B/A/B, profiles/r03_cache_policy_ab.md) */
+    TileKeys cur_t = wk.keys_of(tile, wk.template load_off<0>(tile));
+    Offs no = wk.template load_off<0>(tile + 1u);
     u32x4 d[4];
     load_blk(cur_t, 0u, d);
     uint32_t b = 0;
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
          * every outstanding load, this round's prefetch included); while this
          * tile still has blocks it re-reads the next tile's words, which
          * keeps the per-round load count fixed */
-        no = wk.load_off(more ? tile + 1u : tile + 2u);
+        no = wk.template load_off<0>(more ? tile + 1u : tile + 2u);
         if (fl_tile) {
             if constexpr (FL > 0) {
                 if (act) {

@@ -409,6 +409,24 @@ def probe_read_gbs(buf, iters: int = 20, stream=None, nt: bool = False) -> float
     return nbytes / (ms.value * 1e-3) / 1e9
 
 
+def probe_mix_gbs(buf, iters: int = 20, stream=None, policy: int = 0) -> float:
+    """Same-run ceiling for a hash kernel's traffic mix: GB/s (bytes read +
+    written) of the nt 16-byte read of `buf` with one streaming 16-byte store
+    per 128 bytes read (nc_gpuhash_probe_mix; policy bit 0 / 1: default-policy
+    loads / stores)."""
+    import torch
+
+    nbytes = (buf.numel() // 16) * 16
+    wbytes = -(-nbytes // 32768) * 4096
+    wout = torch.empty(wbytes, dtype=torch.uint8, device=buf.device)
+    sink = torch.zeros(65536, dtype=torch.int32, device=buf.device)
+    ms = ctypes.c_float(0.0)
+    L.check(L.lib().nc_gpuhash_probe_mix(buf.data_ptr(), nbytes, wout.data_ptr(), wbytes, sink.data_ptr(),
+                                         _stream_handle(stream), policy, iters, ctypes.byref(ms)),
+            "nc_gpuhash_probe_mix")
+    return (nbytes + nbytes // 8) / (ms.value * 1e-3) / 1e9
+
+
 def hash_batch_host(hash_: int | str, keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
     """Synchronous host batch (nc_hashkit_batch): pinned copy -> GPU -> copy back."""
     mode = mode_of(hash_)
