@@ -228,8 +228,10 @@ def test_ketama_lookup_table(gpu, oracle, dist_fixture):
     every reference-built pool, a synthetic pool of 300 servers (48,000
     points, past 2^15 and past the LDS budget), one whose points crowd a few
     16-bit ranges, 256 servers (the u8 server bytes' limit) on exactly 4,800
-    points and 4,801 points (just past the LDS limit), hash tags, against the
-    oracle's server_pool_idx."""
+    points and 4,801 points (just past the LDS limit) and on 1,280 / 1,281
+    (the packed LDS continuum's limit), points sharing their top 24 bits with
+    the keys' hashes (the packed search's full-value fallback), hash tags,
+    against the oracle's server_pool_idx."""
     import torch
 
     from twemproxy_amd import _lib as L
@@ -247,9 +249,18 @@ def test_ketama_lookup_table(gpu, oracle, dist_fixture):
     crowd = np.sort(np.concatenate([rng.integers(0, 1 << 18, size=700), rng.integers(0xfffc0000, 1 << 32, size=700),
                                     rng.integers(0, 1 << 32, size=40)]).astype(np.uint64)).astype(np.uint32)
     pools.append((crowd, rng.integers(0, 9, size=crowd.size).astype(np.uint32), 9))
-    for npts in (4800, 4801):
+    for npts in (4800, 4801, 1280, 1281):
         v = np.sort(rng.integers(0, 1 << 32, size=npts, dtype=np.uint64)).astype(np.uint32)
         pools.append((v, rng.integers(0, 256, size=npts).astype(np.uint32), 256))
+    # the packed LDS continuum compares top 24 bits: points that share them
+    # with the keys' own hashes (below, at and above the hash, and runs of
+    # such points) must resolve on full values
+    near = []
+    for m in (6, 1, 10):
+        h = oracle.batch(m, keys, off)[rng.choice(n, size=100, replace=False)].astype(np.int64)
+        near += [h - 1, h, h + 1, (h & ~0xff) | rng.integers(0, 256, size=h.size), (h & ~0xff) | 0xff]
+    near = np.unique(np.clip(np.concatenate(near), 0, (1 << 32) - 1)).astype(np.uint32)[:1280]
+    pools.append((near, rng.integers(0, 200, size=near.size).astype(np.uint32), 200))
     try:
         for vals, idx, nserver in pools:
             cd = t.continuum_device(idx, vals)
@@ -258,8 +269,9 @@ def test_ketama_lookup_table(gpu, oracle, dist_fixture):
                     want = oracle.server_idx_batch(m, 0, vals, idx, nserver, tag, keys, off)
                     # grouped + 65536 / 4096 table in L2, grouped + bucket index over the L2 continuum,
                     # grouped + LDS continuum (256 / 512-key tiles), policy
+                    # (bit 27: the 5-byte LDS continuum where the packed one fits)
                     for var in ((1 << 30) | (1 << 24), (1 << 30) | (1 << 23), (1 << 30) | (1 << 25),
-                                (1 << 30) | (1 << 26), 1 << 30, 0):
+                                (1 << 30) | (1 << 26), (1 << 30) | (1 << 27), 1 << 30, 0):
                         L.lib().nc_gpuhash_set_tuning(0, 0, var)
                         got = t.server_idx_device(m, "ketama", kd, od, cd, nserver, hash_tag=tag, shape=shape)
                         torch.cuda.synchronize()

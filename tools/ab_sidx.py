@@ -16,7 +16,13 @@ sys.path.insert(0, os.path.dirname(HERE))
 PIPES = {"policy": 0, "ring": 1 << 28, "workgroup": 1 << 29, "grouped": 1 << 30, "grouped3": (1 << 30) | (2 << 21),
          "grouped1": (1 << 30) | (1 << 21), "grouped_lut16": (1 << 30) | (1 << 24), "grouped_lut12": (1 << 30) | (1 << 23), "grouped512": (1 << 30) | (1 << 26),
          "workgroup_bkt": (1 << 29) | (1 << 25), "grouped_bkt": (1 << 30) | (1 << 25),
-         "grouped3_bkt": (1 << 30) | (2 << 21) | (1 << 25)}
+         "grouped3_bkt": (1 << 30) | (2 << 21) | (1 << 25),
+         # ketama pools of <= 1280 points: the packed LDS continuum (512-key tiles, 3 sets by default, or 8),
+         # and the 5-byte one it replaces (bit 27)
+         "grouped8": (1 << 30) | (3 << 21), "grouped_5b": (1 << 30) | (1 << 27),
+         # DIAGNOSTIC (fnv1a_64, packed continuum): no hash_tag code / no search (outputs are hashes) / neither
+         "diag_notag": (1 << 30) | (1 << 19), "diag_nosearch": (1 << 30) | (2 << 19),
+         "diag_bare": (1 << 30) | (3 << 19)}
 GRIDS = {}  # name -> grid cap (--grids: workgroup pipeline at these caps)
 
 

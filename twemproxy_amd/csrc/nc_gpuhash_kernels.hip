@@ -539,7 +539,8 @@ __device__ __forceinline__ void full_barrier()
     asm volatile("" ::: "memory");
 }
 
-constexpr int kDistNone = -1, kDistKetama = 0, kDistModula = 1, kDistPre = 3, kDistKetamaLut = 4, kDistKetamaLds = 5;
+constexpr int kDistNone = -1, kDistKetama = 0, kDistModula = 1, kDistPre = 3, kDistKetamaLut = 4, kDistKetamaLds = 5,
+              kDistKetamaLdsPacked = 6;
 
 /* server_pool_idx parameters of one launch (ignored for kDistNone) */
 struct WrDist {
@@ -683,6 +684,46 @@ __device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const 
     return idx[lo == n ? 0u : lo];
 }
 
+/* The same over a PACKED LDS continuum, one word per point: the value's top
+ * 24 bits over the server index (w = v & ~255 | server, pools of <= 256
+ * servers), followed by copies of w[0..3] (so position n reads as the wrap to
+ * point 0). 4 bytes a point keep a 1280-point pool inside the grouped
+ * pipeline's four workgroups per CU. A 512-entry u16 bucket index over the
+ * hash's top 9 bits (~2.5 points a bucket) starts a SCAN four points at a
+ * time (two ds_read2_b32): most keys resolve in two LDS round trips (index,
+ * candidates) instead of a binary search's five. The scan compares h >> 8;
+ * only when the found point shares h's top 24 bits is the answer ambiguous,
+ * and that lane walks the run of such points comparing full values from the
+ * continuum in global memory (cont: {server, value} pairs) — about one key
+ * in 13000 for 1280 points. */
+__device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, const uint16_t *bkt16,
+                                                           const uint32_t *cont, uint32_t n, uint32_t h)
+{
+    const uint32_t b = h >> 23;
+    const uint32_t hk = h >> 8;
+    uint32_t lo = bkt16[b];
+    const uint32_t end = b == 511u ? n : bkt16[b + 1u];
+    uint32_t pos, cand;
+    for (;;) {
+        const uint32_t c0 = w[lo], c1 = w[lo + 1u], c2 = w[lo + 2u], c3 = w[lo + 3u];
+        const uint32_t m = end - lo; /* points of the bucket from lo */
+        /* the bucket is sorted: count its points below h among these four */
+        const uint32_t k = (uint32_t)(m > 0u && (c0 >> 8) < hk) + (uint32_t)(m > 1u && (c1 >> 8) < hk) +
+                           (uint32_t)(m > 2u && (c2 >> 8) < hk) + (uint32_t)(m > 3u && (c3 >> 8) < hk);
+        if (k < 4u) {
+            pos = lo + k;
+            cand = k == 0u ? c0 : (k == 1u ? c1 : (k == 2u ? c2 : c3));
+            break;
+        }
+        lo += 4u; /* all four inside the bucket and below h */
+    }
+    if (pos < n && (cand >> 8) == hk) { /* rare: full values decide */
+        while (pos < n && (w[pos] >> 8) == hk && cont[2u * pos + 1u] < h) pos++;
+        cand = w[pos];
+    }
+    return cand & 0xffu;
+}
+
 /* lower bound of v over the continuum values (no wrap) */
 __device__ __forceinline__ uint32_t cont_lower_bound(const uint32_t *c, uint32_t n, uint32_t v)
 {
@@ -712,6 +753,7 @@ constexpr int wg_dist()
            : ((VAR >> 12) & 7) == 2 ? kDistModula
            : ((VAR >> 12) & 7) == 3 ? kDistKetamaLut
            : ((VAR >> 12) & 7) == 4 ? kDistKetamaLds
+           : ((VAR >> 12) & 7) == 5 ? kDistKetamaLdsPacked
                                     : kDistNone;
 }
 
@@ -723,13 +765,15 @@ __device__ __forceinline__ uint32_t wg_value(const Src &src, typename Src::pos_t
     if constexpr (D == kDistNone) {
         return hash_key<MODE, VAR>(src, p, len, tab);
     } else {
-        if (dist.tag != 0u) tag_trim(src, p, len, dist.tag & 0xffu, (dist.tag >> 8) & 0xffu);
+        if constexpr ((VAR & 256) == 0) { /* VAR bit 8: DIAGNOSTIC, no hash_tag code */
+            if (dist.tag != 0u) tag_trim(src, p, len, dist.tag & 0xffu, (dist.tag >> 8) & 0xffu);
+        }
         uint32_t h = 0u;
         if (len != 0u) h = hash_key<MODE, VAR>(src, p, len, tab);
         const uint32_t *c = dist.cont;
         const uint32_t n = dist.ncont;
-        if constexpr (D == kDistKetamaLds) {
-            return h; /* the caller searches its LDS continuum (ketama_find_lds) */
+        if constexpr (D == kDistKetamaLds || D == kDistKetamaLdsPacked) {
+            return h; /* the caller searches its LDS continuum (ketama_find_lds[_packed]) */
         } else if constexpr (D == kDistModula) {
             return c[2u * (h % n)]; /* nc_modula.c:153 */
         } else if constexpr (D == kDistKetamaLut) {
@@ -1118,7 +1162,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p)
  * Iteration t (after the top barrier: slab(t), offsets(t+1 .. t+D-1) and
  * perm(t) in LDS): pending stores of tile t-1; DMA offsets(t+D) and
  * slab(t+D-1); wave 0 sorts tile t+1; every wave hashes its group of tile t. */
-template <int D, bool CS, int TK>
+template <int D, bool CS, int TK, int RSV = 0>
 struct GsLds {
     static_assert(D == 2 || D == 3, "two or three slab buffers");
     static_assert(TK == 256 || TK == 512, "four or eight waves");
@@ -1129,7 +1173,9 @@ struct GsLds {
     static constexpr uint32_t kFixed = kNOff * kOffSlot + kPermBytes + 4 * 64 + 4 * 256 + 16 + kResBytes;
     /* 8 / 7 workgroups of four waves per CU; 4 of eight (1024-key tiles of
      * sixteen waves, two per CU, measured 40 % slower) */
-    static constexpr uint32_t kBudget = TK == 512 ? 40960 : (D == 2 ? 20480 : 23392);
+    /* RSV: bytes left to dynamic LDS (a packed ketama continuum) within the
+     * same per-workgroup budget */
+    static constexpr uint32_t kBudget = (TK == 512 ? 40960 : (D == 2 ? 20480 : 23392)) - RSV;
     static constexpr uint32_t kCap = ((kBudget - kFixed) / D) & ~15u;
     static constexpr uint32_t kOffs = D * kCap;
     static constexpr uint32_t kPerm = kOffs + kNOff * kOffSlot;
@@ -1247,13 +1293,12 @@ __device__ __forceinline__ void gs_sort(const uint8_t *slot, uint32_t cnt, uint3
     for (int q = 0; q < KPL; q++) gs_ds_write_b16(perm + 2u * (b[q] + rk[q]), (uint32_t)KPL * lane + (uint32_t)q);
 }
 
-template <int MODE, int VAR, int D, bool CS, int TK>
-__global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restrict__ keys_base,
-                                                        const uint64_t *__restrict__ off, uint64_t delta,
-                                                        uint64_t nkeys, uint32_t *__restrict__ out, uint64_t ntiles,
-                                                        WrDist dist)
+template <int MODE, int VAR, int D, bool CS, int TK, int RSV>
+__device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, const uint64_t *__restrict__ off,
+                                        uint64_t delta, uint64_t nkeys, uint32_t *__restrict__ out, uint64_t ntiles,
+                                        const WrDist &dist)
 {
-    using G = GsLds<D, CS, TK>;
+    using G = GsLds<D, CS, TK, RSV>;
     constexpr int kAux = 2; /* nt: read-once streams */
     __shared__ __attribute__((aligned(16))) uint8_t smem[G::kBytes];
     /* kDistKetamaLds: the continuum's values (u32[ncont]) then servers
@@ -1331,14 +1376,42 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
     if (t < 256u) {
         if constexpr (uses_crc_table<MODE>())
             tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
-        if constexpr (wg_dist<VAR>() == kDistKetama || wg_dist<VAR>() == kDistKetamaLds)
-            tab[t] = cont_lower_bound(dist.cont, dist.ncont, t << 24);
+        if constexpr (wg_dist<VAR>() == kDistKetama) tab[t] = cont_lower_bound(dist.cont, dist.ncont, t << 24);
     }
     if constexpr (wg_dist<VAR>() == kDistKetamaLds) {
         uint8_t *ci = reinterpret_cast<uint8_t *>(gs_cont + dist.ncont);
         for (uint32_t i = t; i < dist.ncont; i += TK) {
             gs_cont[i] = dist.cont[2u * i + 1u];
             ci[i] = (uint8_t)dist.cont[2u * i];
+        }
+        /* the 256 bucket starts from the staged values (as the packed form's
+         * below), not by 256 binary searches over global memory */
+        __syncthreads();
+        const uint32_t n = dist.ncont;
+        for (uint32_t i = t; i < n; i += TK) {
+            const uint32_t cb = gs_cont[i] >> 24;
+            for (uint32_t bb = i == 0u ? 0u : (gs_cont[i - 1u] >> 24) + 1u; bb <= cb; bb++) tab[bb] = i;
+            if (i == n - 1u)
+                for (uint32_t bb = cb + 1u; bb < 256u; bb++) tab[bb] = n;
+        }
+    } else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked) {
+        for (uint32_t i = t; i < dist.ncont + 4u; i += TK) {
+            const uint32_t j = i < dist.ncont ? i : (i - dist.ncont) % dist.ncont; /* the wrap copies */
+            gs_cont[i] = (dist.cont[2u * j + 1u] & ~0xffu) | (dist.cont[2u * j] & 0xffu);
+        }
+        /* the u16[512] bucket starts (in the table's 1 KiB) from the staged
+         * words, not by 512 binary searches over global memory (eleven
+         * dependent L2 round trips in every workgroup's prologue): point i
+         * starts the buckets after its predecessor's up to its own, the last
+         * point ends the rest at n */
+        __syncthreads();
+        uint16_t *bkt16 = reinterpret_cast<uint16_t *>(tab);
+        const uint32_t n = dist.ncont;
+        for (uint32_t i = t; i < n; i += TK) {
+            const uint32_t cb = gs_cont[i] >> 23;
+            for (uint32_t bb = i == 0u ? 0u : (gs_cont[i - 1u] >> 23) + 1u; bb <= cb; bb++) bkt16[bb] = (uint16_t)i;
+            if (i == n - 1u)
+                for (uint32_t bb = cb + 1u; bb < 512u; bb++) bkt16[bb] = (uint16_t)n;
         }
     }
 
@@ -1450,6 +1523,8 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
             if constexpr (wg_dist<VAR>() == kDistKetamaLds)
                 h = ketama_find_lds(gs_cont, reinterpret_cast<const uint8_t *>(gs_cont + dist.ncont), tab, dist.ncont,
                                     h);
+            else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked && (VAR & 128) == 0) /* bit 7: DIAGNOSTIC */
+                h = ketama_find_lds_packed(gs_cont, reinterpret_cast<const uint16_t *>(tab), dist.cont, dist.ncont, h);
 
             if constexpr (CS) {
                 gs_ds_write_b32(lds_base + G::kRes + (it & 1u) * 4u * TK + 4u * i, h);
@@ -1474,6 +1549,29 @@ __global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restric
         if (pend_idx != ~0ull) out[pend_idx] = pend_h;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
+}
+
+template <int MODE, int VAR, int D, bool CS, int TK, int RSV = 0>
+__global__ __launch_bounds__(TK) void nc_hash_kernel_gs(const uint8_t *__restrict__ keys_base,
+                                                        const uint64_t *__restrict__ off, uint64_t delta,
+                                                        uint64_t nkeys, uint32_t *__restrict__ out, uint64_t ntiles,
+                                                        WrDist dist)
+{
+    gs_body<MODE, VAR, D, CS, TK, RSV>(keys_base, off, delta, nkeys, out, ntiles, dist);
+}
+
+/* The same with a dynamic-LDS reserve (the packed ketama continuum): its
+ * budget is set for four 512-key workgroups per CU, so the waves must fit
+ * eight per SIMD (<= 64 VGPRs; unconstrained, the dispatch's registers take
+ * it to 71 and three workgroups) */
+template <int MODE, int VAR, int D, bool CS, int TK, int RSV>
+__global__ __launch_bounds__(TK, 8) void nc_hash_kernel_gs_rsv(const uint8_t *__restrict__ keys_base,
+                                                             const uint64_t *__restrict__ off, uint64_t delta,
+                                                             uint64_t nkeys, uint32_t *__restrict__ out,
+                                                             uint64_t ntiles, WrDist dist)
+{
+    static_assert(TK == 512 && RSV > 0, "the reserve form is for 512-key tiles");
+    gs_body<MODE, VAR, D, CS, TK, RSV>(keys_base, off, delta, nkeys, out, ntiles, dist);
 }
 
 /* ---------------- register-staged pipeline (variant bit 5) ----------------
@@ -2261,6 +2359,9 @@ constexpr int kVarGsortCs = 1 << 27; /* its hashes stored once per tile, 16 byte
 constexpr int kVarGsort512 = 1 << 26; /* with kVarGsortCs: 512-key tiles, eight waves (length octiles) */
 constexpr int kVarGsortIssue = 1 << 28; /* A/B: the grouped tile's DMAs issued before the previous tile's store */
 constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline stages in LDS (5 B each) */
+constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 4 wrap copies), beside four 512-key
+                                            workgroups per CU */
+constexpr int kVarNoPacked = 1 << 27; /* server_idx A/B: the 5-byte LDS continuum even where the packed one fits */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2398,13 +2499,14 @@ hipError_t launch_mode(const uint8_t *base, const uint64_t *off, uint64_t delta,
 /* One grouped-workgroup launch (variant bit 25): a persistent grid of
  * `sets` resident sets of workgroups (bits 21-22: 6, 1, 3, 8), so
  * workgroups whose tiles ran short hand their slots to new ones. */
-template <int MODE, int VAR, int D, bool CS = false, int TK = 256>
+template <int MODE, int VAR, int D, bool CS = false, int TK = 256, int RSV = 0>
 hipError_t launch_gs(const uint8_t *base, const uint64_t *off, uint64_t delta, uint64_t nkeys, uint32_t *out,
                      hipStream_t stream, int var, const WrDist &dist = WrDist{nullptr, 0u, 0u, nullptr},
                      size_t dyn_lds = 0)
 {
-    void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist) =
-        nc_hash_kernel_gs<MODE, VAR, D, CS, TK>;
+    void (*kern)(const uint8_t *, const uint64_t *, uint64_t, uint64_t, uint32_t *, uint64_t, WrDist);
+    if constexpr (RSV > 0) kern = nc_hash_kernel_gs_rsv<MODE, VAR, D, CS, TK, RSV>;
+    else kern = nc_hash_kernel_gs<MODE, VAR, D, CS, TK, RSV>;
     /* occupancy per instantiation and dynamic LDS size (the LDS continuum's) */
     static uint64_t occ = 0;
     const int per_cu = cached_occupancy(&occ, kern, TK, dyn_lds, 4);
@@ -2436,6 +2538,13 @@ hipError_t launch_gs_mode(const uint8_t *base, const uint64_t *off, uint64_t del
     if (var & kVarGsortCs) { /* the previous tile's hashes as one coalesced store */
         if ((var & kVarGsortIssue) != 0 && (var & kVarGsort512) != 0) /* A/B: DMAs before the store */
             return launch_gs<MODE, 64, 2, true, 512>(base, off, delta, nkeys, out, stream, var);
+        if constexpr (MODE == NC_GPUHASH_FNV1A_64) { /* DIAGNOSTIC A/B (bits 29-30): occupancy vs slab size */
+            if ((var & kVarGsort512) != 0 && (var & (1 << 29)) != 0) /* 6400 B of unused dynamic LDS */
+                return launch_gs<MODE, 0, 2, true, 512>(base, off, delta, nkeys, out, stream, var,
+                                                        WrDist{nullptr, 0u, 0u, nullptr}, 6400);
+            if ((var & kVarGsort512) != 0 && (var & (1 << 30)) != 0) /* a 5 KiB smaller slab budget */
+                return launch_gs<MODE, 0, 2, true, 512, 5120>(base, off, delta, nkeys, out, stream, var);
+        }
         if (var & kVarGsort512) /* 512-key tiles, eight waves, length octiles */
             return launch_gs<MODE, 0, 2, true, 512>(base, off, delta, nkeys, out, stream, var);
         return d3 ? launch_gs<MODE, 0, 3, true>(base, off, delta, nkeys, out, stream, var)
@@ -2626,6 +2735,30 @@ hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t 
     if constexpr (!uses_crc_table<MODE>()) { /* the crc modes need the workgroup's LDS table slot */
         if (d.gs) {
             const WrDist wd{d.cont, d.ncont, d.tag, d.lut, d.lut_shift};
+            if constexpr (MODE != NC_GPUHASH_MD5) { /* md5's registers do not fit eight waves per SIMD */
+                if (d.kind == 0 && d.lds_cont && d.ncont <= kLdsPackedMax && (d.gs_var & kVarNoPacked) == 0) {
+                    /* packed words within a 5 KiB reserve of the 512-key
+                     * tiles' budget: four workgroups per CU, as without a
+                     * dispatch */
+                    const int sets = (d.gs_var & (3 << 21)) != 0 ? d.gs_var : (d.gs_var | (2 << 21));
+                    constexpr int kR = (kLdsPackedMax + 4) * 4;
+                    const size_t dyn = ((size_t)d.ncont + 4u) * 4u;
+                    if constexpr (MODE == NC_GPUHASH_FNV1A_64) { /* DIAGNOSTIC (tuning bits 19 / 20): what the
+                                                                    dispatch costs — no hash_tag code / no search */
+                        switch ((d.gs_var >> 19) & 3) {
+                        case 1: return launch_gs<MODE, (5 << 12) | 256, 2, true, 512, kR>(base, off, delta, nkeys, out,
+                                                                                            stream, sets, wd, dyn);
+                        case 2: return launch_gs<MODE, (5 << 12) | 128, 2, true, 512, kR>(base, off, delta, nkeys, out,
+                                                                                            stream, sets, wd, dyn);
+                        case 3: return launch_gs<MODE, (5 << 12) | 384, 2, true, 512, kR>(base, off, delta, nkeys, out,
+                                                                                            stream, sets, wd, dyn);
+                        default: break;
+                        }
+                    }
+                    return launch_gs<MODE, 5 << 12, 2, true, 512, kR>(base, off, delta, nkeys, out, stream, sets, wd,
+                                                                       dyn);
+                }
+            }
             if (d.kind == 0 && d.lds_cont) { /* values + u8 servers in dynamic LDS */
                 const size_t vb = (size_t)d.ncont * 4u + (((size_t)d.ncont + 15u) & ~(size_t)15u);
                 if (d.gs_var & kVarGsort512) /* A/B: 512-key tiles (slower: three workgroups per CU) */
@@ -2887,7 +3020,7 @@ extern "C" rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint
     if (tuned & (1 << 29)) wg = true;
     if (tuned & (1 << 28)) wg = false;
     nc_tu::DistArgs d{reinterpret_cast<const uint32_t *>(d_continuum), ncontinuum, 0u, dist, wide, wg, gs,
-                      tuned & ((3 << 21) | (1 << 26)), nullptr, 20u, gs && lds_cont};
+                      tuned & ((3 << 19) | (3 << 21) | (1 << 26) | kVarNoPacked), nullptr, 20u, gs && lds_cont};
     if (hash_tag != nullptr)
         d.tag = (uint32_t)(uint8_t)hash_tag[0] | ((uint32_t)(uint8_t)hash_tag[1] << 8) | (1u << 16);
     /* A/B only: ketama on the workgroup pipelines through a lookup table
