@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r03sidxdiag
 mkdir -p "$O"
 timeout -k 10 400 python3 tools/ab_sidx.py --configs C2 --modes fnv1a_64 --dists ketama --tags none \
-    --pipes policy,grouped_5b,diag_notag,diag_nosearch,diag_bare --rounds 5 > "$O/ab_sidx.jsonl" 2> "$O/ab_sidx.err" \
+    --pipes ${PIPES:-policy,grouped_5b,diag_notag,diag_nosearch,diag_bare} --rounds 5 > "$O/ab_sidx.jsonl" 2> "$O/ab_sidx.err" \
     || { tail -20 "$O/ab_sidx.err"; exit 1; }
 cat "$O/ab_sidx.jsonl"
 timeout -k 10 300 python3 tools/ab.py --configs C2 --modes fnv1a_64 --variants 0 --rounds 5 --iters 10 \

@@ -699,15 +699,15 @@ __device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const 
 __device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, const uint16_t *bkt16,
                                                            const uint32_t *cont, uint32_t n, uint32_t h)
 {
-    const uint32_t b = h >> 23;
     const uint32_t hk = h >> 8;
-    uint32_t lo = bkt16[b];
-    const uint32_t end = b == 511u ? n : bkt16[b + 1u];
+    uint32_t lo = bkt16[h >> 23];
     uint32_t pos, cand;
     for (;;) {
         const uint32_t c0 = w[lo], c1 = w[lo + 1u], c2 = w[lo + 2u], c3 = w[lo + 3u];
-        const uint32_t m = end - lo; /* points of the bucket from lo */
-        /* the bucket is sorted: count its points below h among these four */
+        /* the words are sorted, so those below h come first; past the
+         * bucket's end they are not below h, past n (the wrap copies) they do
+         * not count — no read of the bucket's end needed */
+        const uint32_t m = n - lo;
         const uint32_t k = (uint32_t)(m > 0u && (c0 >> 8) < hk) + (uint32_t)(m > 1u && (c1 >> 8) < hk) +
                            (uint32_t)(m > 2u && (c2 >> 8) < hk) + (uint32_t)(m > 3u && (c3 >> 8) < hk);
         if (k < 4u) {
@@ -715,7 +715,7 @@ __device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, co
             cand = k == 0u ? c0 : (k == 1u ? c1 : (k == 2u ? c2 : c3));
             break;
         }
-        lo += 4u; /* all four inside the bucket and below h */
+        lo += 4u; /* all four below h */
     }
     if (pos < n && (cand >> 8) == hk) { /* rare: full values decide */
         while (pos < n && (w[pos] >> 8) == hk && cont[2u * pos + 1u] < h) pos++;
