@@ -45,8 +45,9 @@ def test_roofline(line):
     assert rf["achieved"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert rf["traffic"] is None  # the committed PMC profiles are of 2^26 keys, not 2^20
     assert rf["alg_bytes_per_launch"] == line["config"]["key_bytes_rank0"] + 12 * (1 << 20)
-    # same-run ceilings: the mix (reads + 12.5 % writes) below the nt read
-    assert 0 < rf["mix_ceiling_gbs"] < rf["read_ceiling_nt_gbs"] * 1.05
+    # the same-run mix ceiling (reads + 12.5 % writes; at this size the
+    # buffer sits in the caches, so no ordering against the read probe)
+    assert rf["mix_ceiling_gbs"] > 0
     assert abs(rf["frac_of_mix_ceiling"] - rf["achieved"] / rf["mix_ceiling_gbs"]) < 1e-3
 
 
