@@ -686,30 +686,27 @@ __device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const 
 
 /* The same over a PACKED LDS continuum, one word per point: the value's top
  * 24 bits over the server index (w = v & ~255 | server, pools of <= 256
- * servers), followed by copies of w[0..3] (so position n reads as the wrap to
- * point 0). 4 bytes a point keep a 1280-point pool inside the grouped
- * pipeline's four workgroups per CU. A 512-entry u16 bucket index over the
- * hash's top 9 bits (~2.5 points a bucket) starts a SCAN four points at a
- * time (two ds_read2_b32): most keys resolve in two LDS round trips (index,
- * candidates) instead of a binary search's five. The scan compares h >> 8;
- * only when the found point shares h's top 24 bits is the answer ambiguous,
- * and that lane walks the run of such points comparing full values from the
- * continuum in global memory (cont: {server, value} pairs) — about one key
- * in 13000 for 1280 points. */
+ * servers), followed by four 0xffffffff sentinels (never below a hash's top
+ * 24 bits, so a scan stops at them without bounds checks). 4 bytes a point
+ * keep a 1280-point pool inside the grouped pipeline's four workgroups per
+ * CU. A 512-entry u16 bucket index over the hash's top 9 bits (~2.5 points a
+ * bucket) starts a SCAN four points at a time (two ds_read2_b32): most keys
+ * resolve in two LDS round trips. The scan compares h >> 8; only when the
+ * found point shares h's top 24 bits is the answer ambiguous, and that lane
+ * walks the run of such points comparing full values from the continuum in
+ * global memory (cont: {server, value} pairs) — about one key in 13000 for
+ * 1280 points. Past the last point the answer wraps to point 0 (w0). */
 __device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, const uint16_t *bkt16,
-                                                           const uint32_t *cont, uint32_t n, uint32_t h)
+                                                           const uint32_t *cont, uint32_t n, uint32_t w0, uint32_t h)
 {
     const uint32_t hk = h >> 8;
     uint32_t lo = bkt16[h >> 23];
     uint32_t pos, cand;
     for (;;) {
         const uint32_t c0 = w[lo], c1 = w[lo + 1u], c2 = w[lo + 2u], c3 = w[lo + 3u];
-        /* the words are sorted, so those below h come first; past the
-         * bucket's end they are not below h, past n (the wrap copies) they do
-         * not count — no read of the bucket's end needed */
-        const uint32_t m = n - lo;
-        const uint32_t k = (uint32_t)(m > 0u && (c0 >> 8) < hk) + (uint32_t)(m > 1u && (c1 >> 8) < hk) +
-                           (uint32_t)(m > 2u && (c2 >> 8) < hk) + (uint32_t)(m > 3u && (c3 >> 8) < hk);
+        /* sorted words: those below h come first */
+        const uint32_t k = (uint32_t)((c0 >> 8) < hk) + (uint32_t)((c1 >> 8) < hk) + (uint32_t)((c2 >> 8) < hk) +
+                           (uint32_t)((c3 >> 8) < hk);
         if (k < 4u) {
             pos = lo + k;
             cand = k == 0u ? c0 : (k == 1u ? c1 : (k == 2u ? c2 : c3));
@@ -717,9 +714,10 @@ __device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, co
         }
         lo += 4u; /* all four below h */
     }
-    if (pos < n && (cand >> 8) == hk) { /* rare: full values decide */
+    if (pos >= n) return w0 & 0xffu; /* past the last point: the wrap */
+    if ((cand >> 8) == hk) { /* rare: full values decide */
         while (pos < n && (w[pos] >> 8) == hk && cont[2u * pos + 1u] < h) pos++;
-        cand = w[pos];
+        cand = pos < n ? w[pos] : w0;
     }
     return cand & 0xffu;
 }
@@ -1373,6 +1371,7 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
 
     uint32_t pad_src = 0u; /* md5: the padding perms' constant in a VGPR (a uniform selector takes the SGPR slot) */
     if constexpr (MODE == NC_GPUHASH_MD5) asm volatile("v_mov_b32 %0, %1" : "=v"(pad_src) : "i"(nc_md5s::kPadSrc));
+    uint32_t pw0 = 0u; /* the packed continuum's first word */
     if (t < 256u) {
         if constexpr (uses_crc_table<MODE>())
             tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
@@ -1395,10 +1394,9 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
                 for (uint32_t bb = cb + 1u; bb < 256u; bb++) tab[bb] = n;
         }
     } else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked) {
-        for (uint32_t i = t; i < dist.ncont + 4u; i += TK) {
-            const uint32_t j = i < dist.ncont ? i : (i - dist.ncont) % dist.ncont; /* the wrap copies */
-            gs_cont[i] = (dist.cont[2u * j + 1u] & ~0xffu) | (dist.cont[2u * j] & 0xffu);
-        }
+        pw0 = (dist.cont[1] & ~0xffu) | (dist.cont[0] & 0xffu); /* point 0, the wrap's answer */
+        for (uint32_t i = t; i < dist.ncont + 4u; i += TK) /* + four sentinels */
+            gs_cont[i] = i < dist.ncont ? (dist.cont[2u * i + 1u] & ~0xffu) | (dist.cont[2u * i] & 0xffu) : ~0u;
         /* the u16[512] bucket starts (in the table's 1 KiB) from the staged
          * words, not by 512 binary searches over global memory (eleven
          * dependent L2 round trips in every workgroup's prologue): point i
@@ -1524,7 +1522,8 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
                 h = ketama_find_lds(gs_cont, reinterpret_cast<const uint8_t *>(gs_cont + dist.ncont), tab, dist.ncont,
                                     h);
             else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked && (VAR & 128) == 0) /* bit 7: DIAGNOSTIC */
-                h = ketama_find_lds_packed(gs_cont, reinterpret_cast<const uint16_t *>(tab), dist.cont, dist.ncont, h);
+                h = ketama_find_lds_packed(gs_cont, reinterpret_cast<const uint16_t *>(tab), dist.cont, dist.ncont,
+                                           pw0, h);
 
             if constexpr (CS) {
                 gs_ds_write_b32(lds_base + G::kRes + (it & 1u) * 4u * TK + 4u * i, h);
@@ -2359,7 +2358,7 @@ constexpr int kVarGsortCs = 1 << 27; /* its hashes stored once per tile, 16 byte
 constexpr int kVarGsort512 = 1 << 26; /* with kVarGsortCs: 512-key tiles, eight waves (length octiles) */
 constexpr int kVarGsortIssue = 1 << 28; /* A/B: the grouped tile's DMAs issued before the previous tile's store */
 constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline stages in LDS (5 B each) */
-constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 4 wrap copies), beside four 512-key
+constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 4 sentinels), beside four 512-key
                                             workgroups per CU */
 constexpr int kVarNoPacked = 1 << 27; /* server_idx A/B: the 5-byte LDS continuum even where the packed one fits */
 
