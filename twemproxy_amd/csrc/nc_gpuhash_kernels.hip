@@ -699,14 +699,13 @@ __device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const 
 __device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, const uint16_t *bkt16,
                                                            const uint32_t *cont, uint32_t n, uint32_t w0, uint32_t h)
 {
-    const uint32_t hk = h >> 8;
+    const uint32_t hb = h & ~0xffu; /* w >> 8 < h >> 8  <=>  w < hb */
     uint32_t lo = bkt16[h >> 23];
     uint32_t pos, cand;
     for (;;) {
         const uint32_t c0 = w[lo], c1 = w[lo + 1u], c2 = w[lo + 2u], c3 = w[lo + 3u];
         /* sorted words: those below h come first */
-        const uint32_t k = (uint32_t)((c0 >> 8) < hk) + (uint32_t)((c1 >> 8) < hk) + (uint32_t)((c2 >> 8) < hk) +
-                           (uint32_t)((c3 >> 8) < hk);
+        const uint32_t k = (uint32_t)(c0 < hb) + (uint32_t)(c1 < hb) + (uint32_t)(c2 < hb) + (uint32_t)(c3 < hb);
         if (k < 4u) {
             pos = lo + k;
             cand = k == 0u ? c0 : (k == 1u ? c1 : (k == 2u ? c2 : c3));
@@ -715,8 +714,8 @@ __device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, co
         lo += 4u; /* all four below h */
     }
     if (pos >= n) return w0 & 0xffu; /* past the last point: the wrap */
-    if ((cand >> 8) == hk) { /* rare: full values decide */
-        while (pos < n && (w[pos] >> 8) == hk && cont[2u * pos + 1u] < h) pos++;
+    if ((cand ^ hb) < 0x100u) { /* rare, the same top 24 bits: full values decide */
+        while (pos < n && (w[pos] ^ hb) < 0x100u && cont[2u * pos + 1u] < h) pos++;
         cand = pos < n ? w[pos] : w0;
     }
     return cand & 0xffu;
