@@ -1,8 +1,7 @@
 /*
  * Slicing-by-4 crc16 / crc32 / crc32a (src/hashkit/nc_crc16.c:56-66,
  * nc_crc32.c:99-123) for gfx950 kernels that keep the tables in LDS: the
- * direct pipeline (nc_bytes_kernels.hip) and the wave ring
- * (nc_gpuhash_kernels.hip, variant kWrSlice).
+ * direct pipeline (nc_bytes_kernels.hip).
  *
  * Four tables T0..T3 of 256 entries: T0 is the byte table (generated from the
  * polynomials, nc_hash_algo.h), Tk advances Tk-1 by one more zero byte, so a
