@@ -700,7 +700,9 @@ __device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, co
                                                            const uint32_t *cont, uint32_t n, uint32_t w0, uint32_t h)
 {
     const uint32_t hb = h & ~0xffu; /* w >> 8 < h >> 8  <=>  w < hb */
-    uint32_t lo = bkt16[h >> 23];
+    /* clamped: an unsorted continuum (a caller error) could leave a bucket
+     * unwritten; from at most n the scan still ends at the sentinels */
+    uint32_t lo = min((uint32_t)bkt16[h >> 23], n);
     uint32_t pos, cand;
     for (;;) {
         const uint32_t c0 = w[lo], c1 = w[lo + 1u], c2 = w[lo + 2u], c3 = w[lo + 3u];
