@@ -65,6 +65,10 @@ def parse():
     p.add_argument("--no-extra", action="store_true", help="skip every secondary leg")
     p.add_argument("--no-c4", action="store_true", help="skip the C4 shard leg")
     p.add_argument("--cpu-sample", type=int, default=1 << 24, help="keys in the CPU baseline sample")
+    p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                   help="process-group backend for N > 1 (nccl = RCCL; gloo stages the scatter through host memory)")
+    p.add_argument("--same-device", action="store_true",
+                   help="every rank on cuda:0: the one-GPU rehearsal of the N > 1 code (tests/test_gpu_bench_dist.py)")
     return p.parse_args()
 
 
@@ -109,12 +113,15 @@ def timed_steps(t, torch, mode, keys, off, out, steps, warmup, dist_on, shape=No
     return wall, kern_ms
 
 
+COMM_DEV = "cuda"  # where the small all-reduces live: cuda for nccl (RCCL), cpu for gloo
+
+
 def max_over_ranks(torch, x: float, dist_on: bool) -> float:
     if not dist_on:
         return x
     import torch.distributed as dist
 
-    v = torch.tensor([x], dtype=torch.float64, device="cuda")
+    v = torch.tensor([x], dtype=torch.float64, device=COMM_DEV)
     dist.all_reduce(v, op=dist.ReduceOp.MAX)
     return float(v.item())
 
@@ -124,7 +131,7 @@ def sum_over_ranks(torch, x: float, dist_on: bool) -> float:
         return x
     import torch.distributed as dist
 
-    v = torch.tensor([x], dtype=torch.float64, device="cuda")
+    v = torch.tensor([x], dtype=torch.float64, device=COMM_DEV)
     dist.all_reduce(v, op=dist.ReduceOp.SUM)
     return float(v.item())
 
@@ -207,12 +214,28 @@ _digests = None
 
 
 def _load_digests():
+    """{cfg: [entry, ...]}: the full-size entry ("configs") and the reduced
+    sizes the multi-rank rehearsal runs at ("small", keyed by keys per rank)"""
     global _digests
     if _digests is None:
+        _digests = {}
         try:
-            _digests = json.load(open(SHARD_DIGESTS))["configs"]
-        except (OSError, ValueError, KeyError):
-            _digests = {}
+            d = json.load(open(SHARD_DIGESTS))
+        except (OSError, ValueError):
+            return
+        for cfg, e in d.get("configs", {}).items():
+            _digests.setdefault(cfg, []).append(e)
+        for cfg, by_n in d.get("small", {}).items():
+            _digests.setdefault(cfg, []).extend(by_n.values())
+
+
+def digest_ranks(cfg: str, n_per_rank: int, world: int):
+    """per-rank digest records of `cfg` at this size and N, or None"""
+    _load_digests()
+    for e in _digests.get(cfg, []):
+        if e["n_per_rank"] == n_per_rank and str(world) in e["N"]:
+            return e["N"][str(world)]
+    return None
 
 
 def rank_parity(torch, cfg: str, mode: str, out, first: int, nk: int, n_per_rank: int, world: int, rank: int):
@@ -222,11 +245,10 @@ def rank_parity(torch, cfg: str, mode: str, out, first: int, nk: int, n_per_rank
     when this run's sizes or N have no digest. Outside every timed region."""
     import hashlib
 
-    _load_digests()
-    c = _digests.get(cfg)
-    if not c or c["n_per_rank"] != n_per_rank or str(world) not in c["N"]:
+    ranks = digest_ranks(cfg, n_per_rank, world)
+    if ranks is None:
         return "unpinned"
-    want = c["N"][str(world)][rank]
+    want = ranks[rank]
     if want["keys"] != [first, first + nk] or mode not in want:
         return "MISMATCH (key range)"
     got = hashlib.sha256(out[:nk].cpu().numpy().tobytes()).hexdigest()
@@ -343,12 +365,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
+    global COMM_DEV
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     dist_on = world > 1
     if dist_on:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+            COMM_DEV = "cpu"
     import twemproxy_amd as t
     from twemproxy_amd.shard import scatter_shards
 
@@ -377,7 +406,8 @@ def main():
         dist.barrier()
         sc = {"ms": round((time.perf_counter() - t0) * 1e3, 2),
               "root_egress_bytes": int(fk.numel() + fo.numel() * 8) if rank == 0 else 0,
-              "how": "rank 0 -> every rank, one grouped batch_isend_irecv (RCCL point-to-point over xGMI)"}
+              "how": (f"rank 0 -> every rank, one grouped batch_isend_irecv per round of <= 1 GiB pieces "
+                      f"({'RCCL point-to-point over xGMI' if args.backend == 'nccl' else 'gloo, host-staged'})")}
         del fk, fo
         torch.cuda.empty_cache()
         return k_, o_, first_, sc
@@ -519,10 +549,9 @@ def main():
     # the whole C2 batch on rank 0 at N = 1, and the §8e alternative ingest —
     # every rank pulls its own C4 shard H2D from pinned host memory and hashes it
     if not args.no_extra:
-        _load_digests()
         if world == 1 and rank == 0:
             try:
-                d2 = _digests.get("C2", {}).get("N", {}).get("1") if args.nkeys == 1 << 26 else None
+                d2 = digest_ranks("C2", args.nkeys, 1)
                 res["e2e_c2"] = e2e_leg(t, torch, "C2", spec, 0, args.nkeys, "fnv1a_64", dev, d2[0] if d2 else None,
                                         world, rank, dist_on)
             except Exception as e:
@@ -530,7 +559,7 @@ def main():
         if not args.no_c4:
             try:
                 n4 = args.c4_nkeys
-                d4 = _digests.get("C4", {}).get("N", {}).get(str(world)) if n4 == 1 << 25 else None
+                d4 = digest_ranks("C4", n4, world)
                 res["c4_ingest"] = e2e_leg(t, torch, "C4 shard (per rank)", t.CONFIGS["C4"]["spec"], rank * n4, n4, "md5",
                                            dev, d4[rank] if d4 else None, world, rank, dist_on,
                                            chunk=(1 << 20, 1 << 28, 3))

@@ -70,9 +70,44 @@ def sha(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+def digest_sets() -> dict:
+    """label -> (spec, keys, modes) of digests.json: every mode on C1, C2 and
+    C3 (each C2 mode's shape-policy pipeline is checked at 2^26 keys)"""
+    c = hk.CONFIGS
+    return {"C1": (c["C1"]["spec"], c["C1"]["nkeys"], hk.HASH_NAMES),
+            "C2": (c["C2"]["spec"], c["C2"]["nkeys"], hk.HASH_NAMES),
+            "C3": (c["C3"]["spec"], c["C3"]["nkeys"], hk.HASH_NAMES),
+            "C4_prefix_2^20": (c["C4"]["spec"], 1 << 20, ("md5", "crc32")),
+            "C5": (c["C5"]["spec"], c["C5"]["nkeys"], ("fnv1a_64",)),
+            "UNI_0_600": (hk.SynthSpec.uniform(6, 0, 600), 1 << 16, hk.HASH_NAMES)}
+
+
+def digest_entry(ref, spec, n, modes, label, t0) -> dict:
+    kb, ob = hk.synth_host(spec, 0, n)
+    entry = {"spec": spec.__dict__, "nkeys": n, "key_bytes": int(ob[-1]),
+             "sha256_keys": sha(kb[: int(ob[-1])]), "sha256_offsets": sha(ob), "modes": {}}
+    for name in modes:
+        out = ref_batch(ref, hk.HASH_NAMES.index(name), kb, ob)
+        entry["modes"][name] = {"sha256": sha(out), "head": [int(x) for x in out[:8]],
+                                "xor": int(np.bitwise_xor.reduce(out)), "sum": int(out.astype(np.uint64).sum())}
+    print(f"  {label}: {n} keys, {time.time() - t0:.1f}s", flush=True)
+    return entry
+
+
 def main() -> None:
     ref = load_ref()
     t0 = time.time()
+    if len(sys.argv) > 2 and sys.argv[1] == "--digests":
+        # refresh only the named digests.json entries (e.g. --digests C2)
+        path = os.path.join(HERE, "digests.json")
+        digests = json.load(open(path))
+        sets = digest_sets()
+        for label in sys.argv[2:]:
+            spec, n, modes = sets[label]
+            digests[label] = digest_entry(ref, spec, n, modes, label, t0)
+        with open(path, "w") as f:
+            json.dump(digests, f, indent=1)
+        return
 
     # 1. KATs (src/test_all.c:41-60) and the Appendix A pattern table
     apple = {name: int(ref.ref_hash(m, b"apple", 5)) for m, name in enumerate(hk.HASH_NAMES)}
@@ -94,27 +129,7 @@ def main() -> None:
     np.savez_compressed(os.path.join(HERE, "corpus.npz"), keys=buf, offsets=off, expected=exp)
 
     # 3. full-size synthetic configs
-    digests = {}
-
-    def add(cfg, spec, n, modes, label=None):
-        kb, ob = hk.synth_host(spec, 0, n)
-        entry = {"spec": spec.__dict__, "nkeys": n, "key_bytes": int(ob[-1]),
-                 "sha256_keys": sha(kb[: int(ob[-1])]), "sha256_offsets": sha(ob), "modes": {}}
-        for name in modes:
-            out = ref_batch(ref, hk.HASH_NAMES.index(name), kb, ob)
-            entry["modes"][name] = {"sha256": sha(out), "head": [int(x) for x in out[:8]],
-                                    "xor": int(np.bitwise_xor.reduce(out)), "sum": int(out.astype(np.uint64).sum())}
-        digests[label or cfg] = entry
-        print(f"  {label or cfg}: {n} keys, {time.time() - t0:.1f}s", flush=True)
-        del kb, ob
-
-    c = hk.CONFIGS
-    add("C1", c["C1"]["spec"], c["C1"]["nkeys"], hk.HASH_NAMES)
-    add("C2", c["C2"]["spec"], c["C2"]["nkeys"], ("fnv1a_64", "md5", "crc32", "murmur"))
-    add("C3", c["C3"]["spec"], c["C3"]["nkeys"], hk.HASH_NAMES)
-    add("C4", c["C4"]["spec"], 1 << 20, ("md5", "crc32"), label="C4_prefix_2^20")
-    add("C5", c["C5"]["spec"], c["C5"]["nkeys"], ("fnv1a_64",))
-    add("UNI", hk.SynthSpec.uniform(6, 0, 600), 1 << 16, hk.HASH_NAMES, label="UNI_0_600")
+    digests = {label: digest_entry(ref, spec, n, modes, label, t0) for label, (spec, n, modes) in digest_sets().items()}
     with open(os.path.join(HERE, "digests.json"), "w") as f:
         json.dump(digests, f, indent=1)
 

@@ -17,6 +17,13 @@ per (config, mode, N, rank) the key range and the sha256 of the reference's
 u32 outputs over it: tests/golden/shard_digests.json (data only). bench.py
 checks every rank against it outside the timed region; the -m gpu test
 test_shard_setup_n8 checks the N = 8 root set-up on one GPU.
+
+    python tests/golden/make_shard_digests.py --small
+
+adds (or refreshes) only the "small" section: the same records at the
+reduced sizes of SMALL (keys per rank), which the one-GPU multi-rank
+rehearsal of bench.py (tests/test_gpu_bench_dist.py) runs at, so that its
+per-rank parity reads "ok" rather than "unpinned".
 """
 from __future__ import annotations
 
@@ -43,6 +50,7 @@ LEGS = {  # config -> (keys per rank, modes bench.py times on it)
     "C3": (1 << 26, ("fnv1a_64", "crc32", "md5")),
     "C4": (1 << 25, ("md5", "crc32", "fnv1a_64")),
 }
+SMALL = {"C2": (1 << 16,), "C3": (1 << 16,), "C4": (1 << 12,)}
 CHUNK_BYTES = 1 << 30
 
 
@@ -58,42 +66,53 @@ def offsets_all(spec, n: int) -> np.ndarray:
 
 
 def main() -> None:
+    path = os.path.join(HERE, "shard_digests.json")
+    if "--small" in sys.argv[1:]:
+        res = json.load(open(path))
+        res["small"] = {cfg: {str(n): entry(load_ref(), cfg, n, LEGS[cfg][1], 1, time.time()) for n in ns}
+                        for cfg, ns in SMALL.items()}
+        with open(path, "w") as f:
+            json.dump(res, f, indent=1)
+        return
     ref = load_ref()
     threads = min(os.cpu_count() or 1, 16)
     t0 = time.time()
     res = {"source": "oracle/_ref (reference src/hashkit compiled from /root/reference), "
                      "tests/golden/make_shard_digests.py",
            "rule": "twemproxy_amd/shard.py plan_bounds over the N x n_per_rank batch (keys from index 0)",
-           "configs": {}}
-    for cfg, (per_rank, modes) in LEGS.items():
-        spec = hk.CONFIGS[cfg]["spec"]
-        ntot = per_rank * max(NS)
-        off = offsets_all(spec, ntot)
-        outs = {m: np.empty(ntot, dtype=np.uint32) for m in modes}
-        mean = max(1, int(off[-1]) // ntot)
-        step = max(1 << 16, CHUNK_BYTES // mean)
-        for k0 in range(0, ntot, step):
-            n = min(step, ntot - k0)
-            kb, ob = hk.synth_host(spec, k0, n)
-            for m in modes:
-                outs[m][k0: k0 + n] = ref_batch(ref, hk.HASH_NAMES.index(m), kb, ob, threads)
-            del kb, ob
-            print(f"  {cfg}: {k0 + n}/{ntot} keys, {time.time() - t0:.0f}s", flush=True)
-        entry = {"spec": spec.__dict__, "n_per_rank": per_rank, "N": {}}
-        for N in NS:
-            n = per_rank * N
-            kb_ = plan_bounds(torch.from_numpy(off[: n + 1].view(np.int64)), N).tolist()
-            ranks = []
-            for r in range(N):
-                lo, hi = kb_[r], kb_[r + 1]
-                ranks.append({"keys": [lo, hi], "bytes": [int(off[lo]), int(off[hi])],
-                              **{m: hashlib.sha256(outs[m][lo:hi].tobytes()).hexdigest() for m in modes}})
-            entry["N"][str(N)] = ranks
-        res["configs"][cfg] = entry
-        del outs, off
-    with open(os.path.join(HERE, "shard_digests.json"), "w") as f:
+           "configs": {cfg: entry(ref, cfg, per_rank, modes, threads, t0) for cfg, (per_rank, modes) in LEGS.items()}}
+    with open(path, "w") as f:
         json.dump(res, f, indent=1)
     print(f"done in {time.time() - t0:.0f}s")
+
+
+def entry(ref, cfg: str, per_rank: int, modes, threads: int, t0: float) -> dict:
+    """per (N, rank): key range, byte range and sha256 of the reference's
+    outputs, for the N x per_rank batch of cfg"""
+    spec = hk.CONFIGS[cfg]["spec"]
+    ntot = per_rank * max(NS)
+    off = offsets_all(spec, ntot)
+    outs = {m: np.empty(ntot, dtype=np.uint32) for m in modes}
+    mean = max(1, int(off[-1]) // ntot)
+    step = max(1 << 16, CHUNK_BYTES // mean)
+    for k0 in range(0, ntot, step):
+        n = min(step, ntot - k0)
+        kb, ob = hk.synth_host(spec, k0, n)
+        for m in modes:
+            outs[m][k0: k0 + n] = ref_batch(ref, hk.HASH_NAMES.index(m), kb, ob, threads)
+        del kb, ob
+        print(f"  {cfg}: {k0 + n}/{ntot} keys, {time.time() - t0:.0f}s", flush=True)
+    rec = {"spec": spec.__dict__, "n_per_rank": per_rank, "N": {}}
+    for N in NS:
+        n = per_rank * N
+        kb_ = plan_bounds(torch.from_numpy(off[: n + 1].view(np.int64)), N).tolist()
+        ranks = []
+        for r in range(N):
+            lo, hi = kb_[r], kb_[r + 1]
+            ranks.append({"keys": [lo, hi], "bytes": [int(off[lo]), int(off[hi])],
+                          **{m: hashlib.sha256(outs[m][lo:hi].tobytes()).hexdigest() for m in modes}})
+        rec["N"][str(N)] = ranks
+    return rec
 
 
 if __name__ == "__main__":

@@ -253,3 +253,39 @@ def test_device_entry_points_check_their_arguments():
         _check_stream(torch.zeros(8, dtype=torch.uint8))
     with pytest.raises(TypeError):
         _check_stream(torch.zeros(8, dtype=torch.int16))
+
+
+def test_pipe_hash_checks_its_arguments():
+    """Pipe.hash's checks (_check_pinned_batch) run before any DMA: a short
+    `out`, a key buffer without NC_GPUHASH_PAD, wrong dtypes, too few offsets,
+    a missing nkeys beside raw addresses, and unpinned tensors all raise."""
+    import torch
+
+    from twemproxy_amd.hashkit import _check_pinned_batch
+
+    keys_np, off_np = t.pack_keys([b"a", b"bb", b"ccc"])
+    keys = torch.from_numpy(keys_np)
+    off = torch.from_numpy(off_np.astype(np.int64))
+    out = torch.empty(3, dtype=torch.int32)
+    with pytest.raises(ValueError, match="out holds 2"):
+        _check_pinned_batch(keys, off, out[:2], None)
+    with pytest.raises(ValueError, match="NC_GPUHASH_PAD"):
+        _check_pinned_batch(keys[: 6 + L.NC_GPUHASH_PAD - 1], off, out, None)
+    with pytest.raises(TypeError):
+        _check_pinned_batch(keys, off.to(torch.int32), out, None)
+    with pytest.raises(TypeError):
+        _check_pinned_batch(keys.to(torch.int8), off, out, None)
+    with pytest.raises(ValueError, match="4 keys need 5"):
+        _check_pinned_batch(keys, off, out, 4)
+    with pytest.raises(ValueError, match="nkeys is required"):
+        _check_pinned_batch(keys, off_np.ctypes.data, out, None)
+    with pytest.raises(ValueError, match="contiguous"):
+        _check_pinned_batch(keys, off, torch.empty(6, dtype=torch.int32)[::2], None)
+    # the raw-address offsets are read to size the key check
+    with pytest.raises(ValueError, match="NC_GPUHASH_PAD"):
+        _check_pinned_batch(keys[:8], off_np.ctypes.data, out, 3)
+    # everything right but the memory is not page-locked (no GPU here to pin it)
+    with pytest.raises(ValueError, match="page-locked"):
+        _check_pinned_batch(keys, off, out, None)
+    # raw addresses alone: the caller's promise, nothing to check
+    assert _check_pinned_batch(keys_np.ctypes.data, off_np.ctypes.data, 0, 3) == 3

@@ -177,9 +177,40 @@ def test_pinned_pipe_registered_numpy_and_limits(gpu, oracle):
             bout = torch.empty(1, dtype=torch.int32).pin_memory()
             with pytest.raises(t.NcError):
                 p.hash("md5", bk, bo, bout)
+            # good chunks first, then the key no chunk holds: the error comes
+            # back only after every queued chunk finished (pipe_drain), so the
+            # hashes before the failing key are all in `out` already
+            small = [b"s%03d" % i for i in range(200)]
+            mk, mo = t.pack_keys(small + [b"y" * 5000])
+            mkt = torch.from_numpy(mk).pin_memory()
+            mot = torch.from_numpy(mo.astype(np.int64)).pin_memory()
+            mout = torch.zeros(201, dtype=torch.int32).pin_memory()
+            with pytest.raises(t.NcError):
+                p.hash("md5", mkt, mot, mout)
+            assert mout.numpy().view(np.uint32)[:200].tolist() == [t.hash_key(1, k) for k in small]
     finally:
         for a in (keys_np, off_np, out):
             t.host_unregister(a.ctypes.data)
+
+
+def test_pinned_pipe_rejects_short_buffers(gpu):
+    """Pipe.hash on pinned tensors: a short `out` or a key buffer without
+    NC_GPUHASH_PAD raises before any copy; the same tensors, right-sized,
+    hash."""
+    import torch
+
+    keys_np, off_np = t.pack_keys([b"k%d" % i for i in range(100)])
+    keys = torch.from_numpy(keys_np).pin_memory()
+    off = torch.from_numpy(off_np.astype(np.int64)).pin_memory()
+    out = torch.zeros(100, dtype=torch.int32).pin_memory()
+    with t.Pipe(0, 64, 4096, 2) as p:
+        with pytest.raises(ValueError):
+            p.hash("fnv1a_64", keys, off, out[:99])
+        with pytest.raises(ValueError):
+            p.hash("fnv1a_64", keys[: int(off_np[-1])], off, out)
+        assert int(out.abs().sum()) == 0  # nothing was written
+        p.hash("fnv1a_64", keys, off, out)
+    assert out.numpy().view(np.uint32).tolist() == [t.hash_key(6, b"k%d" % i) for i in range(100)]
 
 
 def test_probe_mix_contract():

@@ -81,3 +81,37 @@ def test_plan_bounds_matches_c_shard_bounds():
     off = np.zeros(9, dtype=np.int64)
     np.testing.assert_array_equal(plan_bounds(torch.from_numpy(off), 4).numpy(),
                                   t.shard_bounds(off.astype(np.uint64), 4).astype(np.int64))
+
+
+def test_small_shard_digests_pin_the_oracle():
+    """The reduced-size per-rank digests (from the compiled reference, the
+    multi-rank rehearsal's parity check) agree with the restatement's hashes
+    over the same plan_bounds cut, and bench.py finds them by size and N."""
+    import hashlib
+    import json
+
+    import bench
+    from tests.oracle_lib import Oracle
+
+    oracle = Oracle()
+    small = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "shard_digests.json")))["small"]
+    assert set(small) == {"C2", "C3", "C4"}
+    for cfg, by_n in small.items():
+        spec = t.CONFIGS[cfg]["spec"]
+        for n_s, rec in by_n.items():
+            per = int(n_s)
+            for world, ranks in rec["N"].items():
+                w = int(world)
+                keys, off = t.synth_host(spec, 0, per * w)
+                kb = plan_bounds(torch.from_numpy(off.astype(np.int64)), w).tolist()
+                assert [r["keys"] for r in ranks] == [[kb[i], kb[i + 1]] for i in range(w)]
+                assert bench.digest_ranks(cfg, per, w) == ranks
+                for mode in ("fnv1a_64", "md5", "crc32"):
+                    if mode not in ranks[0]:
+                        continue
+                    h = oracle.batch(t.mode_of(mode), keys, off, threads=2)
+                    for i, r in enumerate(ranks):
+                        got = hashlib.sha256(h[kb[i]: kb[i + 1]].tobytes()).hexdigest()
+                        assert got == r[mode], (cfg, per, w, i, mode)
+    assert bench.digest_ranks("C2", 1 << 26, 8) is not None  # the full-size records stay reachable
+    assert bench.digest_ranks("C2", 12345, 2) is None

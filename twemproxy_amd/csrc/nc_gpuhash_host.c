@@ -569,6 +569,21 @@ static uint64_t pipe_cut(const nc_gpuhash_pipe_t *p, const uint64_t *off, uint64
     return lo;
 }
 
+/* every stream of the pipe idle: no DMA still reads the caller's keys or
+ * offsets, none still writes its out, no kernel still runs. Every exit of
+ * nc_gpuhash_batch_pinned goes through here, so the caller may free or
+ * unregister its buffers as soon as the call returns, error or not. errno is
+ * kept. */
+static hipError_t pipe_drain(nc_gpuhash_pipe_t *p)
+{
+    const int saved = errno;
+    const hipError_t a = hipStreamSynchronize(p->s_h2d);
+    const hipError_t b = hipStreamSynchronize(p->s_comp);
+    const hipError_t c = hipStreamSynchronize(p->s_d2h);
+    errno = saved;
+    return a != hipSuccess ? a : (b != hipSuccess ? b : c);
+}
+
 rstatus_t nc_gpuhash_batch_pinned(nc_gpuhash_pipe_t *p, int mode, const uint8_t *keys, const uint64_t *offsets,
                                   uint64_t nkeys, uint32_t *out, const struct nc_gpuhash_shape *shape, int flags)
 {
@@ -591,7 +606,7 @@ rstatus_t nc_gpuhash_batch_pinned(nc_gpuhash_pipe_t *p, int mode, const uint8_t 
         const int b = (int)(c % (uint64_t)p->depth);
         const uint64_t k1 = pipe_cut(p, offsets, k0, nkeys);
         if (k1 == k0) { /* one key longer than a chunk buffer */
-            hipStreamSynchronize(p->s_d2h);
+            pipe_drain(p);
             errno = ENOMEM;
             return NC_ENOMEM;
         }
@@ -628,13 +643,14 @@ rstatus_t nc_gpuhash_batch_pinned(nc_gpuhash_pipe_t *p, int mode, const uint8_t 
                     (unsigned long long)b0, (unsigned long long)nb, (unsigned long long)o[0], (unsigned long long)o[1],
                     (unsigned long long)ol, (o[0] != offsets[k0] || ol != offsets[k1]) ? " MISMATCH" : "");
             if (o[0] != offsets[k0] || ol != offsets[k1]) {
+                pipe_drain(p);
                 errno = EIO;
                 return NC_ERROR;
             }
         }
         if (nc_gpuhash_batch_device_shaped(mode, (const uint8_t *)((uintptr_t)p->d_keys[b] - b0), p->d_off[b], k1 - k0, p->d_out[b], shp,
                                            p->s_comp) != NC_OK) {
-            hipStreamSynchronize(p->s_d2h);
+            pipe_drain(p);
             return NC_ERROR;
         }
         if (dbg >= 2) {
@@ -650,7 +666,7 @@ rstatus_t nc_gpuhash_batch_pinned(nc_gpuhash_pipe_t *p, int mode, const uint8_t 
         if (e != hipSuccess) break;
         k0 = k1;
     }
-    hipError_t e2 = hipStreamSynchronize(p->s_d2h);
+    hipError_t e2 = pipe_drain(p);
     if (e == hipSuccess) e = e2;
     return e == hipSuccess ? NC_OK : hip_fail(e);
 }

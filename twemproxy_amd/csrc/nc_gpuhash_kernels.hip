@@ -646,10 +646,22 @@ __device__ __forceinline__ uint32_t ketama_find(const uint32_t *c, uint32_t n, u
  * bkt[b] = first point with value >= b << 24 (bkt[256] = n), so the answer
  * for h lies in [bkt[h >> 24], bkt[(h >> 24) + 1]] and the search takes
  * ~log2(n / 256) + 1 steps instead of log2(n) */
+/* [lo, lo + cnt) of bucket b, both ends clamped to n: a bucket index built
+ * over an unsorted continuum (a caller error) can hold a start past n or an
+ * end below its start, and the search must still stay inside the continuum
+ * and end (tests/test_gpu_zz_robustness.py) */
+__device__ __forceinline__ uint32_t bucket_span(const uint32_t *bkt, uint32_t b, uint32_t n, uint32_t &lo)
+{
+    lo = min(bkt[b], n);
+    const uint32_t end = b == 255u ? n : min(bkt[b + 1u], n);
+    return end > lo ? end - lo : 0u;
+}
+
 __device__ __forceinline__ uint32_t ketama_find_bkt(const uint32_t *c, const uint32_t *bkt, uint32_t n, uint32_t h)
 {
     const uint32_t b = h >> 24;
-    uint32_t lo = bkt[b], len = bkt[b + 1u] - lo;
+    uint32_t lo;
+    uint32_t len = bucket_span(bkt, b, n, lo);
     while (len > 0u) {
         const uint32_t half = len >> 1;
         if (c[2u * (lo + half) + 1u] < h) {
@@ -669,9 +681,8 @@ __device__ __forceinline__ uint32_t ketama_find_bkt(const uint32_t *c, const uin
 __device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const uint8_t *idx, const uint32_t *bkt,
                                                     uint32_t n, uint32_t h)
 {
-    const uint32_t b = h >> 24;
-    uint32_t lo = bkt[b];
-    uint32_t cnt = (b == 255u ? n : bkt[b + 1u]) - lo;
+    uint32_t lo;
+    uint32_t cnt = bucket_span(bkt, h >> 24, n, lo);
     while (cnt > 0u) {
         const uint32_t half = cnt >> 1;
         if (vals[lo + half] < h) {
@@ -778,9 +789,8 @@ __device__ __forceinline__ uint32_t wg_value(const Src &src, typename Src::pos_t
         } else if constexpr (D == kDistKetamaLut) {
             return ketama_find_lut(c, dist.lut, dist.lut_shift, n, h);
         } else { /* ketama_dispatch, nc_ketama.c:222-246 */
-            const uint32_t b = h >> 24;
-            uint32_t lo = bkt[b];
-            uint32_t cnt = (b == 255u ? n : bkt[b + 1u]) - lo;
+            uint32_t lo;
+            uint32_t cnt = bucket_span(bkt, h >> 24, n, lo);
             while (cnt > 0u) {
                 const uint32_t half = cnt >> 1;
                 if (c[2u * (lo + half) + 1u] < h) {

@@ -557,15 +557,59 @@ class Pipe:
         """keys / offsets / out: pinned host tensors (torch pin_memory) or
         addresses of pinned memory; uint8 keys readable NC_GPUHASH_PAD bytes
         past offsets[nkeys], int64/uint64 offsets, int32/uint32 out. Blocks
-        until every hash is in `out`."""
+        until every hash is in `out`.
+
+        Tensor arguments are checked (_check_pinned_batch) before any copy
+        starts. A raw address is the caller's promise: nothing behind it can
+        be checked, and `nkeys` must then be given."""
         def addr(x):
             return x if isinstance(x, int) else x.data_ptr()
 
-        if nkeys is None:
-            nkeys = offsets.numel() - 1
+        nkeys = _check_pinned_batch(keys, offsets, out, nkeys)
         L.check(self._lib.nc_gpuhash_batch_pinned(self._h, mode_of(hash_), addr(keys), addr(offsets), nkeys,
                                                    addr(out), _shape_arg(shape), 0),
                 "nc_gpuhash_batch_pinned")
+
+
+def _check_pinned_batch(keys, offsets, out, nkeys: int | None) -> int:
+    """Argument checks of Pipe.hash (nc_gpuhash_batch_pinned DMAs
+    offsets[nkeys] + NC_GPUHASH_PAD bytes from `keys` and 4 * nkeys bytes into
+    `out`, so a short tensor would be read or written past its end): dtypes,
+    contiguity, sizes, then page-locked host memory. Returns nkeys."""
+    import torch
+
+    def tensor(x, name, dtypes):
+        if isinstance(x, int):
+            return None
+        if x.dtype not in dtypes:
+            raise TypeError(f"{name} must be {' or '.join(str(d) for d in dtypes)}, not {x.dtype}")
+        if x.device.type != "cpu" or not x.is_contiguous() or x.dim() != 1:
+            raise ValueError(f"{name} must be a contiguous 1-D host tensor")
+        return x
+
+    u64 = getattr(torch, "uint64", torch.int64)
+    u32 = getattr(torch, "uint32", torch.int32)
+    k = tensor(keys, "keys", (torch.uint8,))
+    o = tensor(offsets, "offsets", (torch.int64, u64))
+    w = tensor(out, "out", (torch.int32, u32))
+    if nkeys is None:
+        if o is None:
+            raise ValueError("nkeys is required when offsets is a raw address")
+        nkeys = o.numel() - 1
+    if nkeys < 0 or (o is not None and o.numel() < nkeys + 1):
+        raise ValueError(f"offsets holds {None if o is None else o.numel()} entries; {nkeys} keys need {nkeys + 1}")
+    if w is not None and w.numel() < nkeys:
+        raise ValueError(f"out holds {w.numel()} hashes; {nkeys} keys need {nkeys}")
+    if k is not None and nkeys > 0:
+        if o is not None:
+            end = int(o[nkeys].item())
+        else:
+            end = ctypes.c_uint64.from_address(offsets + 8 * nkeys).value
+        _check_key_room(k.numel(), end)
+    for x, name in ((k, "keys"), (o, "offsets"), (w, "out")):
+        if x is not None and x.numel() and not x.is_pinned():
+            raise ValueError(f"{name} must be page-locked (pin_memory() or nc_gpuhash_host_register)")
+    return nkeys
 
 
 def host_register(ptr: int, nbytes: int) -> None:
