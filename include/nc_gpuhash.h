@@ -306,6 +306,25 @@ rstatus_t nc_gpuhash_host_unregister(void *ptr);
 rstatus_t nc_gpuhash_shard_bounds(const uint64_t *offsets, uint64_t nkeys, uint32_t nshards,
                                   uint64_t *key_bounds);
 
+/* ---- 5. fragment plan (the batch sites' second half) ----
+ * What memcache_fragment_retrieval (src/proto/nc_memcache.c:1283-1370) and
+ * redis_fragment_argx (src/proto/nc_redis.c:2804-2898) make of ONE
+ * multi-key request once its keys' server indices are known (batched:
+ * nc_gpuhash_server_idx_device over the request's keys; the reference calls
+ * msg_backend_idx per key, src/nc_message.c:461-467): one fragment per
+ * distinct server, fragments in ascending server order (the reference walks
+ * sub_msgs[0 .. nserver)), keys in request order inside each. For keys
+ * 0 .. nkeys-1 with server indices sidx[]: frag_seq[i] = key i's fragment
+ * (the position of r->frag_seq[i] in the fragment queue), frag_server[f] =
+ * fragment f's server, frag_nkeys[f] = its key count; the frag_* arrays hold
+ * min(nkeys, nserver) entries. The reference does not fragment a one-key
+ * request (memcache_should_fragment, src/proto/nc_memcache.c:104-118;
+ * redis_fragment, src/proto/nc_redis.c:2903): that stays the caller's test.
+ * Returns the number of fragments (0 for no keys), or -1 with errno EINVAL
+ * (NULL buffers, nserver 0, a server index >= nserver). Host code, no GPU. */
+int nc_gpuhash_frag_plan(const uint32_t *sidx, uint32_t nkeys, uint32_t nserver, uint32_t *frag_seq,
+                         uint32_t *frag_server, uint32_t *frag_nkeys);
+
 /* ---- info ---- */
 /* Number of visible GPUs (0 when none); never initialises more than HIP's
  * device query does. */

@@ -90,3 +90,39 @@ def server_idx_cases(doc, dist_fixture):
         else:
             vals, idx = None, np.array(p["modula"]["indices"], np.uint32)
         yield c, p, vals, idx
+
+
+def frag_requests(doc, redis: bool):
+    """the fragment fixture's requests of one protocol, and the pipelined
+    stream of all of them (request r at stream[bounds[r]:bounds[r + 1]])"""
+    reqs = [base64.b64decode(r) for r in doc["fragments"]["redis_b64" if redis else "memcache_b64"]]
+    bounds = np.concatenate([[0], np.cumsum([len(r) for r in reqs])]).astype(np.int64)
+    return reqs, b"".join(reqs), bounds
+
+
+def frag_pool(case, dist_fixture):
+    """(continuum values or None, indices, nserver) of a fragment case's pool"""
+    p = dist_fixture["pools"][case["pool"]]
+    if case["dist"] == 0:
+        return np.array(p["ketama"]["values"], np.uint32), np.array(p["ketama"]["indices"], np.uint32), len(p["names"])
+    return None, np.array(p["modula"]["indices"], np.uint32), len(p["names"])
+
+
+def check_fragments(case, redis: bool, reqs, keys_by_req, sidx_by_req):
+    """every request of one fixture case: the server of each key, the key ->
+    fragment map and the fragments' bytes against the reference's
+    msg->fragment (twemproxy_amd.fragment, nc_gpuhash_frag_plan)"""
+    from twemproxy_amd.fragment import fragments
+
+    want = case["redis" if redis else "memcache"]
+    nserver = int(case["nserver"])
+    for r, (req, keys, sidx) in enumerate(zip(reqs, keys_by_req, sidx_by_req)):
+        w = want[r]
+        tag = f"{'redis' if redis else 'memcache'} request {r} mode {case['mode']} dist {case['dist']}"
+        assert [int(x) for x in sidx] == w["sidx"], tag
+        seq, frags = fragments(redis, req, keys, sidx, nserver)
+        if not w["frags_b64"]:
+            assert seq is None and frags == [], tag
+            continue
+        assert [int(x) for x in seq] == w["frag_seq"], tag
+        assert frags == [base64.b64decode(f) for f in w["frags_b64"]], tag

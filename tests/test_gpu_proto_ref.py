@@ -73,3 +73,36 @@ def test_server_idx_matches_reference(gpu, dist_fixture, wide, pipe):
                                           err_msg=f"mode {c['mode']} {dist} tag {c['tag']!r} pipe {pipe}")
     finally:
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
+@pytest.mark.parametrize("redis", [False, True], ids=["memcache", "redis"])
+def test_fragments_on_device_match_reference(gpu, dist_fixture, redis):
+    """The batch site on the device: one pipelined stream of multi-key
+    requests parsed by the device parser into a key CSR, the fused
+    server_pool_idx over all of its keys in ONE launch, then the fragment
+    plan (nc_gpuhash_frag_plan) and the fragments' bytes per request, against
+    what the reference's own memcache_fragment / redis_fragment made of each
+    request (tests/golden/proto_ref.json "fragments", every case)."""
+    import torch
+
+    reqs, stream, _ = P.frag_requests(DOC, redis)
+    Parser = t.RedisParser if redis else t.McParser
+    kw = {"max_key_len": DOC["mbuf_data_size"]} if redis else {}
+    with Parser(max_bytes=1 << 20, max_reqs=1 << 12, max_keys=1 << 14, **kw) as p:
+        kd, od, kreq, status, info = p.parse(dev(stream))
+        torch.cuda.synchronize()
+        assert info["first_error"] == len(reqs) and info["consumed"] == len(stream), info
+        kr = kreq.cpu().numpy()[: info["nkeys"]]
+        o = od.cpu().numpy()
+        kb = kd.cpu().numpy()
+        kbytes = [kb[o[i]: o[i + 1]].tobytes() for i in range(info["nkeys"])]
+        by_req = [np.flatnonzero(kr == r) for r in range(len(reqs))]
+        for case in DOC["fragments"]["cases"]:
+            vals, idx, nserver = P.frag_pool(case, dist_fixture)
+            cd = t.continuum_device(idx, vals) if vals is not None else t.continuum_device(idx)
+            got = t.server_idx_device(case["mode"], t.DIST_NAMES[case["dist"]], kd, od, cd, nserver,
+                                      hash_tag=case["tag"].encode() or None)
+            torch.cuda.synchronize()
+            sidx = got.cpu().numpy().view(np.uint32)
+            P.check_fragments(case, redis, reqs, [[kbytes[j] for j in sel] for sel in by_req],
+                              [sidx[sel] for sel in by_req])

@@ -49,3 +49,41 @@ def test_oracle_server_idx_matches_reference(oracle, dist_fixture):
                                       err_msg=f"mode {c['mode']} dist {c['dist']} tag {c['tag']!r}")
         n += 1
     assert n == len(DOC["server_idx"]["cases"]) >= 200
+
+
+@pytest.mark.parametrize("ci", range(8))
+@pytest.mark.parametrize("redis", [False, True], ids=["memcache", "redis"])
+def test_fragments_match_reference(oracle, dist_fixture, redis, ci):
+    """The batch site end to end on the host: the oracle's parser and
+    server_pool_idx over a pipelined stream of multi-key requests, then
+    nc_gpuhash_frag_plan and twemproxy_amd.fragment's copies, against what
+    the reference's own memcache_fragment / redis_fragment made of each
+    request (tests/golden/proto_ref.json "fragments")."""
+    import twemproxy_amd as t
+
+    case = DOC["fragments"]["cases"][ci]
+    reqs, stream, bounds = P.frag_requests(DOC, redis)
+    parse = oracle.redis_parse if redis else oracle.mc_parse
+    ks, kl, kr, st, info = parse(stream)
+    assert info["first_error"] == len(reqs) and info["consumed"] == len(stream)
+    kbytes = [stream[int(s): int(s) + int(n)] for s, n in zip(ks, kl)]
+    keys, off = t.pack_keys(kbytes)
+    vals, idx, nserver = P.frag_pool(case, dist_fixture)
+    sidx = oracle.server_idx_batch(case["mode"], case["dist"], vals, idx, nserver, case["tag"].encode() or None,
+                                   keys, off)
+    by_req = [np.flatnonzero(kr == r) for r in range(len(reqs))]
+    P.check_fragments(case, redis, reqs, [[kbytes[j] for j in sel] for sel in by_req],
+                      [sidx[sel] for sel in by_req])
+
+
+def test_frag_plan_contract():
+    from twemproxy_amd.fragment import frag_plan
+
+    seq, srv, cnt = frag_plan([5, 1, 5, 3, 1], 8)
+    assert seq.tolist() == [2, 0, 2, 1, 0] and srv.tolist() == [1, 3, 5] and cnt.tolist() == [2, 1, 2]
+    seq, srv, cnt = frag_plan([], 4)
+    assert seq.size == 0 and srv.size == 0
+    import twemproxy_amd as t
+
+    with pytest.raises(t.NcError):
+        frag_plan([0, 4], 4)  # a server index >= nserver

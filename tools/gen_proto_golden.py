@@ -14,6 +14,12 @@
   server_idx: server_pool_idx (src/nc_server.c:647-700) of tagged keys over
     the tests/golden/dist.json pools, every hash mode, ketama and modula,
     hash_tag none / "{}" / "$$" / "ab".
+  fragments: multi-key requests — memcache get / gets, redis mget / del /
+    touch / unlink / mset — each fragmented by the reference's own
+    msg->fragment (memcache_fragment, src/proto/nc_memcache.c:1283-1389;
+    redis_fragment, src/proto/nc_redis.c:2804-2924) from a client connection
+    owned by a dist.json pool: per key the server msg_backend_idx picked and
+    its fragment (frag_seq), and every fragment's bytes as sent.
 
 Data only (inputs and the reference's outputs): run here, commit the JSON.
     make -C oracle ref-proto && python tools/gen_proto_golden.py
@@ -85,6 +91,12 @@ class Ref:
         lib.rp_parse_one.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_uint32] + [ctypes.c_void_p] * 6 + \
             [ctypes.c_uint32]
         lib.rp_type_name.argtypes = [ctypes.c_int32, ctypes.c_char_p, ctypes.c_uint32]
+        lib.rp_fragment.restype = ctypes.c_int
+        lib.rp_fragment.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                    ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                    ctypes.c_uint32, ctypes.c_void_p]
         lib.rp_server_idx.restype = ctypes.c_int
         lib.rp_server_idx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
@@ -113,7 +125,8 @@ class Ref:
         while pos < len(stream):
             window = stream[pos: pos + self.mbuf_data]
             r = self.parse_one(redis, window)
-            r["keys"] = [[s + pos, e + pos] for s, e in r["keys"]]
+            # [-1, -1]: a span the reference pushed outside the request (COMMAND, LOLWUT)
+            r["keys"] = [[s + pos, e + pos] if s != 0xFFFFFFFF else [-1, -1] for s, e in r["keys"]]
             r["start"] = pos
             reqs.append(r)
             if r["result"] != "OK" or r["consumed"] == 0:
@@ -134,6 +147,27 @@ class Ref:
                                     kb.ctypes.data, off.ctypes.data, len(keys), out.ctypes.data)
         assert rc == 0
         return out.tolist()
+
+
+    def fragment(self, redis: bool, req: bytes, mode, dist, names, weights, tag: bytes):
+        nb = [n.encode() for n in names]
+        arr = (ctypes.c_char_p * len(nb))(*nb)
+        lens = np.array([len(n) for n in nb], np.uint32)
+        w = np.array(weights, np.uint32)
+        kcap, pcap, fcap = 4096, 1 << 20, 1024
+        sidx, fseq = np.zeros(kcap, np.uint32), np.zeros(kcap, np.uint32)
+        payload, plen = np.zeros(pcap, np.uint8), np.zeros(fcap, np.uint32)
+        nfrag = ctypes.c_uint32()
+        nk = self.lib.rp_fragment(1 if redis else 0, req, len(req), mode, dist, arr, lens.ctypes.data, w.ctypes.data,
+                                  len(nb), tag, len(tag), sidx.ctypes.data, fseq.ctypes.data, kcap,
+                                  payload.ctypes.data, pcap, plen.ctypes.data, fcap, ctypes.byref(nfrag))
+        assert nk > 0, req[:80]
+        frags, pos = [], 0
+        for n in plen[: nfrag.value].tolist():
+            frags.append(b64(payload[pos: pos + n].tobytes()))
+            pos += n
+        return {"sidx": sidx[:nk].tolist(), "frag_seq": fseq[:nk].tolist() if nfrag.value else [],
+                "frags_b64": frags}
 
 
 def b64(b: bytes) -> str:
@@ -167,6 +201,29 @@ def tagged_keys(rng, n):
     return out
 
 
+def frag_requests(rng):
+    """multi-key requests the fragment loops split: memcache get / gets, redis
+    mget / del / touch / unlink (one key per argument) and mset (key, value
+    pairs); 1..48 keys of tagged_keys shape, values binary"""
+    mc, rd = [], []
+    pool = [k for k in tagged_keys(rng, 400) if k and b" " not in k]
+    for i in range(48):
+        nk = 1 + (i % 48) if i < 40 else int(rng.integers(2, 48))
+        ks = [pool[int(j)] for j in rng.integers(0, len(pool), size=nk)]
+        mc.append((b"gets" if i % 5 == 4 else b"get") + b"".join(b" " + k for k in ks) + b"\r\n")
+        cmd = [b"mget", b"del", b"touch", b"unlink", b"mset"][i % 5]
+        if cmd == b"mset":
+            args = []
+            for k in ks[:24]:
+                v = rng.integers(0, 256, size=int(rng.integers(0, 20)), dtype=np.uint8).tobytes()
+                args += [k, v]
+        else:
+            args = ks
+        rd.append(b"*%d\r\n$%d\r\n%s\r\n" % (len(args) + 1, len(cmd), cmd) +
+                  b"".join(b"$%d\r\n%s\r\n" % (len(a), a) for a in args))
+    return mc, rd
+
+
 def main():
     from tests import redis_gen as G
 
@@ -196,6 +253,16 @@ def main():
                     sidx.append({"pool": pi, "mode": mode, "dist": d, "tag": tag.decode(),
                                  "idx": ref.server_idx(mode, d, p["names"], p["weights"], tag, keys)})
     doc["server_idx"] = {"keys_b64": [b64(k) for k in keys], "cases": sidx}
+    mc_reqs, rd_reqs = frag_requests(np.random.default_rng(7070))
+    fcases = []
+    for pi, mode, d, tag in ((0, 6, 0, b""), (1, 6, 0, b"{}"), (2, 1, 0, b""), (1, 10, 1, b""), (2, 3, 0, b"{}"),
+                             (0, 9, 1, b"$$"), (1, 11, 0, b""), (2, 0, 1, b"{}")):
+        p = dist["pools"][pi]
+        fcases.append({"pool": pi, "mode": mode, "dist": d, "tag": tag.decode(), "nserver": len(p["names"]),
+                       "memcache": [ref.fragment(False, r, mode, d, p["names"], p["weights"], tag) for r in mc_reqs],
+                       "redis": [ref.fragment(True, r, mode, d, p["names"], p["weights"], tag) for r in rd_reqs]})
+    doc["fragments"] = {"memcache_b64": [b64(r) for r in mc_reqs], "redis_b64": [b64(r) for r in rd_reqs],
+                        "cases": fcases}
     with open(OUT, "w") as f:
         json.dump(doc, f, separators=(",", ":"))
     nreq = sum(len(s["reqs"]) for s in doc["redis"]) + sum(len(s["reqs"]) for s in doc["memcache"])

@@ -130,6 +130,10 @@ SIGNATURES = {
          ctypes.c_int, ctypes.POINTER(ctypes.c_float)],
     ),
     "nc_gpuhash_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "nc_gpuhash_frag_plan": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+    ),
     "nc_gpuhash_ctx_create": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
     "nc_gpuhash_ctx_destroy": (None, [ctypes.c_void_p]),
     "nc_gpuhash_ctx_set_zero_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),

@@ -137,8 +137,8 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane4 = nc_slice::copy_of<kCopies>(lane); /* this lane's table copy */
     const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
-    uint64_t tile = 0; /* local tile index */
-    const uint64_t tlast = tiles.n;
+    uint32_t tile = 0; /* local tile index */
+    const uint32_t tlast = tiles.n;
     if (tile >= tlast) return;
     Walker<IL> wk;
     wk.init(keys, off, nkeys, tiles, lane);

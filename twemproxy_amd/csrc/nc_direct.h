@@ -38,7 +38,14 @@ constexpr uint32_t kLineImage = 64u * 128u; /* one 128-byte line of each of a ti
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void *base, uint64_t nbytes)
 {
-    const uint32_t n = nbytes > 0xffffffffull ? 0xffffffffu : (uint32_t)nbytes;
+    /* the clamp by the high dword, on the scalar unit: hipcc turns a plain
+     * C form back into a 64-bit unsigned compare, which gfx9 can only do on
+     * the VALU (the SALU has no 64-bit less-than). nbytes is wave-uniform. */
+    uint32_t n;
+    asm("s_cmp_lg_u32 %1, 0\n\ts_cselect_b32 %0, -1, %2"
+        : "=s"(n)
+        : "s"((uint32_t)(nbytes >> 32)), "s"((uint32_t)nbytes)
+        : "scc");
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)n, kRsrcWord3);
 }
 
@@ -60,22 +67,26 @@ struct Offs {
  * Consecutive (IL false, S = 1: `chunk` neighbouring tiles per wave) or
  * interleaved over the grid (IL, S = every wave of the launch), in which case
  * the resident waves read neighbouring tiles at any moment instead of regions
- * `chunk` tiles apart. Either way the grid covers every tile once. */
+ * `chunk` tiles apart. Either way the grid covers every tile once. Every
+ * index is 32-bit: the direct pipeline takes batches of < 2^32 keys (the
+ * launcher checks), so tiles, key indices and their compares stay on the
+ * scalar unit. */
 template <bool IL>
 struct Tiles {
-    uint64_t base, S, n;
-    __device__ __forceinline__ uint64_t at(uint64_t j) const { return IL ? base + j * S : base + j; }
+    uint32_t base, S, n;
+    __device__ __forceinline__ uint32_t at(uint32_t j) const { return IL ? base + j * S : base + j; }
 };
 
 template <bool IL>
-__device__ __forceinline__ Tiles<IL> wave_tiles(uint64_t ntiles, uint32_t chunk, uint32_t waves_per_block,
+__device__ __forceinline__ Tiles<IL> wave_tiles(uint64_t ntiles64, uint32_t chunk, uint32_t waves_per_block,
                                                 uint32_t wave)
 {
-    const uint64_t w = (uint64_t)blockIdx.x * waves_per_block + wave;
+    const uint32_t ntiles = (uint32_t)ntiles64; /* < 2^26 */
+    const uint32_t w = blockIdx.x * waves_per_block + wave;
     Tiles<IL> t;
     if constexpr (IL) {
         t.base = w;
-        t.S = (uint64_t)gridDim.x * waves_per_block;
+        t.S = gridDim.x * waves_per_block;
         t.n = w < ntiles ? (ntiles - w + t.S - 1u) / t.S : 0u;
     } else {
         t.base = w * chunk;
@@ -90,10 +101,10 @@ template <bool IL>
 struct Walker {
     const uint8_t *keys;
     const uint64_t *off;
-    uint64_t nkeys;
+    uint32_t nkeys;  /* < 2^32 (the launchers check) */
     uint64_t kbytes; /* readable bytes from keys: off[nkeys] + NC_GPUHASH_PAD */
     Tiles<IL> tiles; /* this wave's tiles; local indices below */
-    uint64_t tlast;  /* = tiles.n */
+    uint32_t tlast;  /* = tiles.n */
     uint32_t lane;
 
     __device__ __forceinline__ void init(const uint8_t *k, const uint64_t *o, uint64_t n, const Tiles<IL> &tl,
@@ -101,7 +112,7 @@ struct Walker {
     {
         keys = k;
         off = o;
-        nkeys = n;
+        nkeys = (uint32_t)n;
         kbytes = off[n] + (uint64_t)NC_GPUHASH_PAD;
         tiles = tl;
         tlast = tl.n;
@@ -109,7 +120,7 @@ struct Walker {
     }
 
     /* first key of local tile tl */
-    __device__ __forceinline__ uint64_t key0(uint64_t tl) const { return tiles.at(tl) * 64u; }
+    __device__ __forceinline__ uint32_t key0(uint32_t tl) const { return tiles.at(tl) * 64u; }
 
     /* offsets of local tile tl; this wave's last tile again past its range, so
      * that every round issues the same loads (keys past nkeys read as 0).
@@ -118,10 +129,10 @@ struct Walker {
      * crcs nothing.) AUX: the loads' cache policy — streaming for the byte
      * kernels, the default for md5 (profiles/r03_cache_policy_ab.md). */
     template <int AUX = kAuxNt>
-    __device__ __forceinline__ Offs load_off(uint64_t tl) const
+    __device__ __forceinline__ Offs load_off(uint32_t tl) const
     {
-        const uint64_t k0 = key0(tl < tlast ? tl : tlast - 1u);
-        const rsrc_t r = make_rsrc(off + k0, (nkeys + 1u - k0) * 8u);
+        const uint32_t k0 = key0(tl < tlast ? tl : tlast - 1u);
+        const rsrc_t r = make_rsrc(off + k0, ((uint64_t)(nkeys - k0) + 1u) * 8u);
         Offs o;
         o.s = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u), 0, AUX);
         o.e = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u + 8u), 0, AUX);
@@ -129,13 +140,16 @@ struct Walker {
         return o;
     }
 
-    __device__ __forceinline__ TileKeys keys_of(uint64_t tl, const Offs &o) const
+    __device__ __forceinline__ TileKeys keys_of(uint32_t tl, const Offs &o) const
     {
         TileKeys t;
         t.s0 = o.s0;
         t.srel = o.s - (uint32_t)o.s0;
         t.len = o.e - o.s;
-        t.valid = key0(tl) + lane < nkeys;
+        /* the tile's key count, uniform and 32-bit (lane < it: one VALU compare) */
+        const uint32_t k0 = key0(tl);
+        const uint32_t nv = k0 < nkeys ? nkeys - k0 : 0u;
+        t.valid = lane < nv;
         return t;
     }
 

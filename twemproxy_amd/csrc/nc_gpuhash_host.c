@@ -66,6 +66,47 @@ int nc_gpuhash_device_count(void)
 
 /* ---------------- shard planning ---------------- */
 
+int nc_gpuhash_frag_plan(const uint32_t *sidx, uint32_t nkeys, uint32_t nserver, uint32_t *frag_seq,
+                         uint32_t *frag_server, uint32_t *frag_nkeys)
+{
+    if ((nkeys != 0 && (sidx == NULL || frag_seq == NULL || frag_server == NULL || frag_nkeys == NULL)) ||
+        nserver == 0) {
+        errno = EINVAL;
+        return -1;
+    }
+    /* the distinct servers, kept sorted in frag_server (at most
+     * min(nkeys, nserver) of them: a request's keys touch few servers) */
+    uint32_t nf = 0;
+    for (uint32_t i = 0; i < nkeys; i++) {
+        const uint32_t s = sidx[i];
+        if (s >= nserver) {
+            errno = EINVAL;
+            return -1;
+        }
+        uint32_t lo = 0, hi = nf;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (frag_server[mid] < s) lo = mid + 1; else hi = mid;
+        }
+        if (lo == nf || frag_server[lo] != s) {
+            memmove(frag_server + lo + 1, frag_server + lo, (size_t)(nf - lo) * sizeof(*frag_server));
+            frag_server[lo] = s;
+            nf++;
+        }
+    }
+    for (uint32_t f = 0; f < nf; f++) frag_nkeys[f] = 0;
+    for (uint32_t i = 0; i < nkeys; i++) {
+        uint32_t lo = 0, hi = nf;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (frag_server[mid] < sidx[i]) lo = mid + 1; else hi = mid;
+        }
+        frag_seq[i] = lo;
+        frag_nkeys[lo]++;
+    }
+    return (int)nf;
+}
+
 rstatus_t nc_gpuhash_shard_bounds(const uint64_t *offsets, uint64_t nkeys, uint32_t nshards,
                                   uint64_t *key_bounds)
 {

@@ -76,9 +76,8 @@ __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__re
         w[0] = (len & 63u) == 0u ? 0x80u : 0u;
         w[14] = len << 3;
         w[15] = len >> 29;
-        /* (the generic block: md5_tail_final_a costs this kernel three VGPRs,
-         * one wave per SIMD) */
-        __builtin_nontemporal_store(md5_block_final_a(st, w), out + idx);
+        /* words 1..13 are zero: folded into the steps' constants */
+        __builtin_nontemporal_store(md5_tail_final_a(st, w), out + idx);
     }
     q.head = (q.head + n) & (kQ - 1u);
     q.count -= n;
@@ -94,7 +93,7 @@ __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__re
  * past off[nkeys]. A tile of 64 keys spans less than 4 GiB.
  */
 template <bool LDS, bool IL, int FL = 0>
-__global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__restrict__ keys,
+__global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
                                                            uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
 {
@@ -108,8 +107,8 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
      * and the hardware dispatcher balances the waves (no persistent grid to
      * size from an occupancy estimate) */
     const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
-    uint64_t tile = 0; /* local tile index */
-    const uint64_t tlast = tiles.n;
+    uint32_t tile = 0; /* local tile index */
+    const uint32_t tlast = tiles.n;
     if (tile >= tlast) return;
     Queue q{qmem + wave * kQWords * kQ, 0u, 0u};
     Walker<IL> wk;
@@ -126,50 +125,54 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
      * C2 0.787 -> 0.772 ms in an A/B/A/B, profiles/r03_cache_policy_ab.md) */
     TileKeys cur_t = wk.keys_of(tile, wk.template load_off<0>(tile));
     Offs no = wk.template load_off<0>(tile + 1u);
-    u32x4 d[4];
-    load_blk(cur_t, 0u, d);
+    u32x4 da[4], db[4];
+    load_blk(cur_t, 0u, da);
     uint32_t b = 0;
     uint32_t st[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
     uint32_t pad_src; /* kPadSrc in a VGPR: a uniform selector takes the perm's SGPR slot */
     asm volatile("v_mov_b32 %0, %1" : "=v"(pad_src) : "i"(kPadSrc));
 
-    /* One round: block b of every key of the tile that has one. Its message
-     * words are padded out of `d` first; then `d` receives the next round's
-     * loads (block b+1 of this tile if any key has one, else block 0 of the
-     * next tile, whose offsets are in `no`), which fly during the 64 steps. */
-    for (;;) {
+    /* One round: block b of every key of the tile that has one, from `cur`
+     * (loaded during the previous round). Its message words are padded out of
+     * `cur` first; then the next round's loads (block b+1 of this tile if any
+     * key has one, else block 0 of the next tile, whose offsets are in `no`)
+     * go to the OTHER register set `nxt` and fly during the 64 steps. Two
+     * sets, alternating (the loop below runs rounds in pairs), so that a
+     * message word taken as loaded — a fixed-length key's data words, a full
+     * block — is read by the steps in place: with one set it had to be copied
+     * out before the next round's loads could land there (24 v_mov per round
+     * in the fixed-length form). */
+    auto round = [&](u32x4 (&cur)[4], u32x4 (&nxt)[4]) __attribute__((always_inline)) {
         const bool more = __ballot(cur_t.valid && cur_t.len > 64u * (b + 1u)) != 0ull;
         const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
         const int32_t rem = (int32_t)cur_t.len - 64 * (int32_t)b; /* key bytes from this block's start */
         const uint32_t len = cur_t.len;
         const bool act = cur_t.valid && rem > 0;
-        uint32_t w[16];
-        if constexpr (LDS) wk.read_img(img, d); /* this round's block, DMA'd during the previous round */
-        const u32x4 (&cur)[4] = d;
+        if constexpr (LDS) wk.read_img(img, cur); /* this round's block, DMA'd during the previous round */
         /* FL: a tile whose keys all have FL bytes (checked: the shape only
          * picks the instantiation) takes its data words as loaded, the
-         * boundary word by one constant perm, and constants for the rest */
+         * boundary word by one constant perm, and constants for the rest.
+         * Every form pads `cur` in place: the steps read it as it stands. */
         bool fl_tile = false;
         if constexpr (FL > 0) fl_tile = __ballot(cur_t.valid && cur_t.len != (uint32_t)FL) == 0ull;
         if (fl_tile) {
-            if constexpr (FL > 0) {
-#pragma unroll
-                for (int t = 0; t < FL / 4; t++) w[t] = cur[t >> 2][t & 3];
-                if constexpr (FL % 4 != 0) {
-                    constexpr uint32_t bnd = FL % 4 == 1 ? kBoundary1 : (FL % 4 == 2 ? kBoundary2 : kBoundary3);
-                    w[FL / 4] = __builtin_amdgcn_perm(cur[(FL / 4) >> 2][(FL / 4) & 3], pad_src, bnd);
-                }
+            if constexpr (FL > 0 && FL % 4 != 0) {
+                constexpr uint32_t bnd = FL % 4 == 1 ? kBoundary1 : (FL % 4 == 2 ? kBoundary2 : kBoundary3);
+                cur[(FL / 4) >> 2][(FL / 4) & 3] = __builtin_amdgcn_perm(cur[(FL / 4) >> 2][(FL / 4) & 3], pad_src, bnd);
             }
         } else if (act) {
-            msg_words(cur, rem < 64 ? rem : 64, pad_src, w);
+            pad_block(cur, rem < 64 ? rem : 64, pad_src);
             const bool fin = rem <= 55; /* the bit length fits behind the pad */
             if (fin) {
-                w[14] = len << 3;
-                w[15] = len >> 29;
+                cur[3][2] = len << 3;
+                cur[3][3] = len >> 29;
             }
         }
+        uint32_t w[16];
+#pragma unroll
+        for (int t = 0; t < 16; t++) w[t] = cur[t >> 2][t & 3];
         if constexpr (LDS) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the image's reads are done */
-        load_blk(more ? cur_t : nxt_t, more ? b + 1u : 0u, d);
+        load_blk(more ? cur_t : nxt_t, more ? b + 1u : 0u, nxt);
         /* offsets two tiles ahead, straight into `no` (consumed above: a copy
          * of a register whose load is in flight would make hipcc wait for
          * every outstanding load, this round's prefetch included); while this
@@ -214,7 +217,7 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
                 q.w[2 * kQ + slot] = st[2];
                 q.w[3 * kQ + slot] = st[3];
                 q.w[4 * kQ + slot] = len;
-                q.w[5 * kQ + slot] = (uint32_t)(wk.key0(tile) + lane);
+                q.w[5 * kQ + slot] = wk.key0(tile) + lane;
             }
             q.count += (uint32_t)__builtin_popcountll(tm);
             if (q.count >= 64u) run_tail(q, lane, out);
@@ -232,6 +235,11 @@ __global__ __launch_bounds__(256) void nc_md5_direct_kernel(const uint8_t *__res
             st[2] = NC_MD5_C0;
             st[3] = NC_MD5_D0;
         }
+    };
+    for (;;) {
+        round(da, db);
+        if (tile >= tlast) break;
+        round(db, da);
         if (tile >= tlast) break;
     }
     while (q.count != 0u) run_tail(q, lane, out);
@@ -254,8 +262,8 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
-    uint64_t tile = 0; /* local tile index */
-    const uint64_t tlast = tiles.n;
+    uint32_t tile = 0; /* local tile index */
+    const uint32_t tlast = tiles.n;
     if (tile >= tlast) return;
     Walker<IL> wk;
     wk.init(keys, off, nkeys, tiles, lane);
@@ -269,14 +277,16 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
     asm volatile("v_mov_b32 %0, %1" : "=v"(pad_src) : "i"(kPadSrc));
 
     /* one 64-byte block holding rem (> 0) of the key's remaining bytes */
-    auto block = [&](const u32x4 (&d)[4], int32_t rem) __attribute__((always_inline)) {
-        uint32_t w[16];
-        msg_words(d, rem < 64 ? rem : 64, pad_src, w);
+    auto block = [&](u32x4 (&d)[4], int32_t rem) __attribute__((always_inline)) {
+        pad_block_u(d, rem < 64 ? rem : 64, pad_src); /* in place */
         const bool fin = rem <= 55;
         if (fin) {
-            w[14] = cur_t.len << 3;
-            w[15] = cur_t.len >> 29;
+            d[3][2] = cur_t.len << 3;
+            d[3][3] = cur_t.len >> 29;
         }
+        uint32_t w[16];
+#pragma unroll
+        for (int t = 0; t < 16; t++) w[t] = d[t >> 2][t & 3];
         uint32_t v[4] = {st[0], st[1], st[2], st[3]};
         md5_steps(v, w, std::make_integer_sequence<int, 61>{});
         if (fin) {

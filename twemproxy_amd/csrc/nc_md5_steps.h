@@ -23,17 +23,25 @@ constexpr uint32_t kT[64] = {NC_MD5_ROUNDS(NC_MD5_KT)};
 constexpr int kM[64] = {NC_MD5_ROUNDS(NC_MD5_KM)};
 constexpr int kS[64] = {NC_MD5_ROUNDS(NC_MD5_KS)};
 
+/* The round function of step I. H (b ^ c ^ d) is one v_bitop3_b32 (truth
+ * table 0x96), where hipcc's own choice is two dependent v_xor_b32: 16 VALU
+ * per block fewer. F, G and I already compile to one v_bitop3 each. */
+template <int I>
+__device__ __forceinline__ uint32_t md5_f(uint32_t b, uint32_t c, uint32_t d)
+{
+    if constexpr (I < 16) return NC_MD5_F(b, c, d);
+    else if constexpr (I < 32) return NC_MD5_G(b, c, d);
+    else if constexpr (I < 48) return __builtin_amdgcn_bitop3_b32(b, c, d, 0x96);
+    else return NC_MD5_I(b, c, d);
+}
+
 /* Step I updates one of the four state words: a, d, c, b in turn. */
 template <int I>
 __device__ __forceinline__ void md5_step(uint32_t (&v)[4], const uint32_t (&w)[16])
 {
     constexpr int u = (4 - (I & 3)) & 3;
     const uint32_t b = v[(u + 1) & 3], c = v[(u + 2) & 3], d = v[(u + 3) & 3];
-    uint32_t f;
-    if constexpr (I < 16) f = NC_MD5_F(b, c, d);
-    else if constexpr (I < 32) f = NC_MD5_G(b, c, d);
-    else if constexpr (I < 48) f = NC_MD5_H(b, c, d);
-    else f = NC_MD5_I(b, c, d);
+    const uint32_t f = md5_f<I>(b, c, d);
     /* w + T by a VOP2 literal add off the step's dependency chain, then
      * a + (w + T) + f by one v_add3_u32: five VALU instructions per step, no
      * scalar s_mov of T, and a four-op chain f -> add3 -> rotate -> add
@@ -84,11 +92,7 @@ __device__ __forceinline__ void md5_step_fl(uint32_t (&v)[4], const uint32_t (&w
     if constexpr (fl_const<FL>(k)) {
         constexpr int u = (4 - (I & 3)) & 3;
         const uint32_t b = v[(u + 1) & 3], c = v[(u + 2) & 3], d = v[(u + 3) & 3];
-        uint32_t f;
-        if constexpr (I < 16) f = NC_MD5_F(b, c, d);
-        else if constexpr (I < 32) f = NC_MD5_G(b, c, d);
-        else if constexpr (I < 48) f = NC_MD5_H(b, c, d);
-        else f = NC_MD5_I(b, c, d);
+        const uint32_t f = md5_f<I>(b, c, d);
         constexpr uint32_t wt = fl_word<FL>(k) + kT[I];
         v[u] = nc_rotl(v[u] + f + wt, kS[I]) + b;
     } else {
@@ -113,11 +117,7 @@ __device__ __forceinline__ void md5_step_tail(uint32_t (&v)[4], const uint32_t (
     if constexpr (k >= 1 && k <= 13) {
         constexpr int u = (4 - (I & 3)) & 3;
         const uint32_t b = v[(u + 1) & 3], c = v[(u + 2) & 3], d = v[(u + 3) & 3];
-        uint32_t f;
-        if constexpr (I < 16) f = NC_MD5_F(b, c, d);
-        else if constexpr (I < 32) f = NC_MD5_G(b, c, d);
-        else if constexpr (I < 48) f = NC_MD5_H(b, c, d);
-        else f = NC_MD5_I(b, c, d);
+        const uint32_t f = md5_f<I>(b, c, d);
         v[u] = nc_rotl(v[u] + f + kT[I], kS[I]) + b;
     } else {
         md5_step<I>(v, w);
@@ -173,16 +173,30 @@ __device__ __forceinline__ uint32_t pad_word(uint32_t d, int32_t y)
     return __builtin_amdgcn_perm(d, kPadSrc, (uint32_t)sel);
 }
 
+/* The message words y0 selector of a key of m (0..64) bytes in its last
+ * data block, per lane: kBoundary[m % 4] + (m / 4) * kStep, no branches */
+__device__ __forceinline__ int32_t pad_y0(uint32_t m)
+{
+    const uint32_t r = m & 3u;
+    const uint64_t pair = (r & 2u) ? ((uint64_t)kBoundary3 << 32 | kBoundary2) : ((uint64_t)kBoundary1 << 32 | kBoundary0);
+    const uint32_t bnd = (uint32_t)(pair >> (32u * (r & 1u)));
+    return (int32_t)bnd + (int32_t)(m >> 2) * kStep;
+}
+
 /* The 16 message words of a block holding m (1..64) of the key's bytes, the
  * pad byte after them and zeros (no bit length: the caller adds it). When m
  * is the same on every active lane (fixed-length keys) the selectors are
- * wave-uniform and computed on the scalar unit. */
+ * wave-uniform and computed on the scalar unit; when it is 64 on every lane
+ * (a full data block of long keys) the words stay as loaded. */
 typedef unsigned int md5_u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void msg_words(const md5_u32x4 (&d)[4], int32_t m, uint32_t pad_src, uint32_t (&w)[16])
 {
     const int32_t m0 = __builtin_amdgcn_readfirstlane(m);
-    if (__ballot(m != m0) == 0ull) {
+    if (__ballot(m != m0) == 0ull && m0 >= 64) {
+#pragma unroll
+        for (int t = 0; t < 16; t++) w[t] = d[t >> 2][t & 3];
+    } else if (__ballot(m != m0) == 0ull) {
         const uint32_t r = (uint32_t)m0 & 3u;
         const uint32_t bnd = r == 0u ? kBoundary0 : (r == 1u ? kBoundary1 : (r == 2u ? kBoundary2 : kBoundary3));
         const int32_t y0 = (int32_t)bnd + (m0 >> 2) * kStep;
@@ -195,25 +209,48 @@ __device__ __forceinline__ void msg_words(const md5_u32x4 (&d)[4], int32_t m, ui
             w[t] = __builtin_amdgcn_perm(d[t >> 2][t & 3], pad_src, sel);
         }
     } else {
-        const uint32_t r = (uint32_t)m & 3u;
-        /* kBoundary[r] without branches: two 64-bit selects and a shift */
-        const uint64_t pair = (r & 2u) ? ((uint64_t)kBoundary3 << 32 | kBoundary2)
-                                       : ((uint64_t)kBoundary1 << 32 | kBoundary0);
-        const uint32_t bnd = (uint32_t)(pair >> (32u * (r & 1u)));
-        const int32_t y0 = (int32_t)bnd + (m >> 2) * kStep;
+        const int32_t y0 = pad_y0((uint32_t)m);
 #pragma unroll
         for (int t = 0; t < 16; t++) w[t] = pad_word(d[t >> 2][t & 3], y0 - t * kStep);
     }
 }
 
-/* The message words y0 selector of a key of m (0..64) bytes in its last
- * data block, per lane: kBoundary[m % 4] + (m / 4) * kStep, no branches */
-__device__ __forceinline__ int32_t pad_y0(uint32_t m)
+/* The same, IN PLACE in the block's registers, per lane (the direct kernel,
+ * whose steps read the block's own register set): the 16 words are rewritten
+ * where they stand, so the register allocator keeps one set of 16 words. (A
+ * wave-uniform branch with scalar selectors here made hipcc allocate 16 more
+ * VGPRs for it and copy them back: occupancy 8 -> 6 waves per SIMD. Tiles of
+ * one fixed length take the kernel's FL form instead.) */
+__device__ __forceinline__ void pad_block(md5_u32x4 (&d)[4], int32_t m, uint32_t pad_src)
 {
-    const uint32_t r = m & 3u;
-    const uint64_t pair = (r & 2u) ? ((uint64_t)kBoundary3 << 32 | kBoundary2) : ((uint64_t)kBoundary1 << 32 | kBoundary0);
-    const uint32_t bnd = (uint32_t)(pair >> (32u * (r & 1u)));
-    return (int32_t)bnd + (int32_t)(m >> 2) * kStep;
+    const int32_t y0 = pad_y0((uint32_t)m);
+#pragma unroll
+    for (int t = 0; t < 16; t++) d[t >> 2][t & 3] = pad_word(d[t >> 2][t & 3], y0 - t * kStep);
+}
+
+/* pad_block with the wave-uniform cases of msg_words (the line kernel, whose
+ * blocks come from LDS reads, so no load is in flight into d): a length
+ * shared by every lane pads by scalar selectors, a full block (m = 64 on
+ * every lane) stays as read — 16 v_perm / v_mov fewer per block of a long
+ * key. */
+__device__ __forceinline__ void pad_block_u(md5_u32x4 (&d)[4], int32_t m, uint32_t pad_src)
+{
+    const int32_t m0 = __builtin_amdgcn_readfirstlane(m);
+    if (__ballot(m != m0) == 0ull) {
+        if (m0 < 64) {
+            const uint32_t r = (uint32_t)m0 & 3u;
+            const uint32_t bnd = r == 0u ? kBoundary0 : (r == 1u ? kBoundary1 : (r == 2u ? kBoundary2 : kBoundary3));
+            const int32_t y0 = (int32_t)bnd + (m0 >> 2) * kStep;
+#pragma unroll
+            for (int t = 0; t < 16; t++) {
+                uint32_t sel;
+                asm("s_max_i32 %0, %1, 0\n\ts_min_i32 %0, %0, %2" : "=&s"(sel) : "s"(y0 - t * kStep), "s"(kKeep));
+                d[t >> 2][t & 3] = __builtin_amdgcn_perm(d[t >> 2][t & 3], pad_src, sel);
+            }
+        }
+    } else {
+        pad_block(d, m, pad_src);
+    }
 }
 
 /* md5 of a key of len bytes at byte p of a dword-readable slab (LDS, or a
