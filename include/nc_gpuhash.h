@@ -300,6 +300,36 @@ rstatus_t nc_gpuhash_batch_pinned(nc_gpuhash_pipe_t *p, int mode, const uint8_t 
 rstatus_t nc_gpuhash_host_register(void *ptr, size_t bytes);
 rstatus_t nc_gpuhash_host_unregister(void *ptr);
 
+/* ---- 3d. small batches with no HIP call per batch: the batch ring ----
+ * One mbuf's keys at a time (the batch site of src/nc_message.c:700-714 and
+ * the fragment loops) without a kernel launch or an event per batch: the
+ * ring's slots live in mapped, coherent host memory and resident worker
+ * workgroups on the GPU poll them (csrc/nc_ring.hip): batch n belongs to lane
+ * n % 2 (one lane when nslots == 1), each lane with its own worker. A submit
+ * copies the spans' bytes into the slot (the mbufs may be recycled on return)
+ * and publishes it with one store; the worker hashes it and writes the hashes
+ * and a completion word back to host memory; poll is one load. A lane's
+ * worker is launched on its first batch, leaves after 10 ms of an empty ring
+ * (or 2 s in any case) and is relaunched by the next submit or poll. Up to
+ * nslots batches in flight, in order within a lane (the two lanes may finish
+ * out of order: poll each ticket). Limits per batch:
+ * max_keys <= 4095 keys, max_key_bytes <= 32768 bytes (two mbufs' worth).
+ * NULL with errno on failure (EINVAL limits, ENODEV no GPU). Thread-safe per
+ * ring (one mutex). */
+typedef struct nc_gpuhash_ring nc_gpuhash_ring_t;
+nc_gpuhash_ring_t *nc_gpuhash_ring_create(int device, uint32_t nslots, uint32_t max_keys, uint64_t max_key_bytes);
+/* stops the workers (they return at their next poll) and frees the ring */
+void nc_gpuhash_ring_destroy(nc_gpuhash_ring_t *r);
+/* submit keypos-style spans; NC_EAGAIN when the next slot's batch is still in
+ * flight, NC_ENOMEM past the limits; *ticket identifies the batch */
+rstatus_t nc_gpuhash_ring_submit_spans(nc_gpuhash_ring_t *r, int mode, const struct nc_keyspan *spans,
+                                       uint32_t nkeys, uint32_t *out, int *ticket);
+/* NC_OK once the batch's hashes are in its `out`, NC_EAGAIN before */
+rstatus_t nc_gpuhash_ring_poll(nc_gpuhash_ring_t *r, int ticket);
+rstatus_t nc_gpuhash_ring_wait(nc_gpuhash_ring_t *r, int ticket);
+/* worker launches so far (the first submit's, and relaunches after idle) */
+uint64_t nc_gpuhash_ring_launches(const nc_gpuhash_ring_t *r);
+
 /* ---- 4. multi-GPU shard planning ----
  * Split keys [0, nkeys) into nshards contiguous ranges with about equal key
  * bytes: key_bounds[g] .. key_bounds[g+1] is shard g (nshards + 1 entries). */

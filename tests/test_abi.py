@@ -289,3 +289,15 @@ def test_pipe_hash_checks_its_arguments():
         _check_pinned_batch(keys, off, out, None)
     # raw addresses alone: the caller's promise, nothing to check
     assert _check_pinned_batch(keys_np.ctypes.data, off_np.ctypes.data, 0, 3) == 3
+
+
+def test_ring_without_gpu_and_bad_limits():
+    """nc_gpuhash_ring_create: EINVAL past its limits (slots, 4095 keys,
+    32 KiB of key bytes), ENODEV without a GPU"""
+    lib = L.lib()
+    for args in ((0, 0, 100, 1000), (0, 4, 4096, 1000), (0, 4, 100, 32769), (0, 4, 0, 1000)):
+        assert not lib.nc_gpuhash_ring_create(*args)
+        assert ctypes.get_errno() == errno.EINVAL
+    if t.device_count() == 0:
+        assert not lib.nc_gpuhash_ring_create(0, 4, 100, 1000)
+        assert ctypes.get_errno() == errno.ENODEV

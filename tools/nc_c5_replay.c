@@ -13,6 +13,8 @@
  * way the fragment loop would.
  *
  * For in-flight depths 1, 2 and 4 (context slots), copy and zero-copy paths,
+ * and depths 1, 2, 4 and 8 of the batch ring (nc_gpuhash_ring: a resident
+ * worker polls mapped host memory, no HIP call per batch),
  * it reports submit->done latency per mbuf and keys/s, and beside them the
  * per-key host hash of the same spans through a hash_t pointer (one core, as
  * the reference's event loop does, src/nc_server.c:643). Every batch is
@@ -186,6 +188,69 @@ int main(int argc, char **argv)
             nc_gpuhash_ctx_destroy(ctx);
             free(outs);
         }
+    }
+    /* the batch ring: the same loop over nc_gpuhash_ring_* */
+    static const int rdepths[] = {1, 2, 4, 8};
+    for (size_t di = 0; di < sizeof(rdepths) / sizeof(rdepths[0]); di++) {
+        const int nslots = rdepths[di];
+        nc_gpuhash_ring_t *ring = nc_gpuhash_ring_create(0, (uint32_t)nslots, maxk, MBUF_DATA);
+        if (!ring) {
+            fprintf(stderr, "ring_create failed\n");
+            return 1;
+        }
+        uint32_t *outs = malloc((size_t)nslots * maxk * sizeof(uint32_t));
+        int tick[8];
+        uint32_t which[8];
+        double t_sub[8];
+        if (!outs) return 1;
+        for (uint32_t i = 0; i < nmb; i++) { /* warm-up (the first submit launches the worker) */
+            int tk;
+            if (nc_gpuhash_ring_submit_spans(ring, NC_GPUHASH_FNV1A_64, mb[i].spans, mb[i].nkeys, outs, &tk) != NC_OK ||
+                nc_gpuhash_ring_wait(ring, tk) != NC_OK)
+                return 1;
+        }
+        uint64_t done_keys = 0, batches = 0, bad = 0;
+        double lat_sum = 0.0;
+        int inflight = 0, head = 0;
+        uint32_t next = 0;
+        const double t0 = now_s(), tend = t0 + seconds;
+        for (;;) {
+            const int stop = now_s() >= tend;
+            if (inflight == nslots || (stop && inflight > 0)) {
+                const int s = head;
+                if (nc_gpuhash_ring_wait(ring, tick[s]) != NC_OK) return 1;
+                lat_sum += now_s() - t_sub[s];
+                const uint32_t *o = outs + (size_t)s * maxk;
+                for (uint32_t k = 0; k < mb[which[s]].nkeys; k++) bad += o[k] != ref[first[which[s]] + k];
+                done_keys += mb[which[s]].nkeys;
+                batches++;
+                head = (head + 1) % nslots;
+                inflight--;
+                continue;
+            }
+            if (stop) break;
+            const int s = (head + inflight) % nslots;
+            const uint32_t bi = next;
+            next = (next + 1) % nmb;
+            t_sub[s] = now_s();
+            if (nc_gpuhash_ring_submit_spans(ring, NC_GPUHASH_FNV1A_64, mb[bi].spans, mb[bi].nkeys,
+                                             outs + (size_t)s * maxk, &tick[s]) != NC_OK) {
+                fprintf(stderr, "ring submit failed\n");
+                return 1;
+            }
+            which[s] = bi;
+            inflight++;
+        }
+        const double el = now_s() - t0;
+        printf("{\"point\": \"gpu\", \"path\": \"ring (resident worker, mapped host memory)\", \"depth\": %d, "
+               "\"batches\": %" PRIu64 ", \"keys_per_batch\": %.1f, \"submit_to_done_us\": %.2f, \"mkeys_s\": %.2f, "
+               "\"mismatches\": %" PRIu64 ", \"worker_launches\": %" PRIu64 "}\n",
+               nslots, batches, (double)done_keys / (double)batches, lat_sum / (double)batches * 1e6,
+               (double)done_keys / el / 1e6, bad, nc_gpuhash_ring_launches(ring));
+        fflush(stdout);
+        if (bad) rc = 2;
+        nc_gpuhash_ring_destroy(ring);
+        free(outs);
     }
     free(first);
     free(ref);

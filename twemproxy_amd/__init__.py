@@ -18,6 +18,7 @@ from .hashkit import (
     McParser,
     Pipe,
     RedisParser,
+    Ring,
     SynthSpec,
     conf_set_hash,
     continuum_device,
@@ -49,5 +50,5 @@ __all__ = [
     "BYTES_FULL", "BYTES_PRINTABLE", "CONFIGS", "DIST_NAMES", "HASH_DEFAULT", "HASH_NAMES", "NMODES",
     "Context", "SynthSpec", "conf_set_hash", "device_count", "hash_batch_device", "hash_batch_host",
     "hash_key", "hash_keys", "ketama_hash", "md5_signature", "mode_of", "pack_keys", "pick_variant", "probe_mix_gbs", "probe_read_gbs", "server_idx_device", "shape_of", "shard_bounds", "continuum_device", "ketama_build_device", "McParser", "RedisParser",
-    "synth_device", "synth_host", "time_batch_device", "Pipe", "host_register", "host_unregister",
+    "synth_device", "synth_host", "time_batch_device", "Pipe", "Ring", "host_register", "host_unregister",
 ]

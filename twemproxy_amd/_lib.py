@@ -130,6 +130,15 @@ SIGNATURES = {
          ctypes.c_int, ctypes.POINTER(ctypes.c_float)],
     ),
     "nc_gpuhash_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "nc_gpuhash_ring_create": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+    "nc_gpuhash_ring_destroy": (None, [ctypes.c_void_p]),
+    "nc_gpuhash_ring_submit_spans": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)],
+    ),
+    "nc_gpuhash_ring_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "nc_gpuhash_ring_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "nc_gpuhash_ring_launches": (ctypes.c_uint64, [ctypes.c_void_p]),
     "nc_gpuhash_frag_plan": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],

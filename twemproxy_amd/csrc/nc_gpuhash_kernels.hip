@@ -2350,15 +2350,15 @@ using nc_tu::g_variant;
 /* Auto-policy choices (variant bits): the workgroup pipeline (bit 16 only
  * marks an explicit choice; it is stripped before launch), the register-staged
  * workgroup pipeline, and the wave ring with 5 KiB / 4 KiB slab slots. */
-constexpr int kVarWorkgroup = 1 << 16;
-constexpr int kVarRegStaged = 32;
-constexpr int kVarRingP5 = 128 | (3 << 8);
-constexpr int kVarRingP4 = 128;
-constexpr int kVarSorted = 1 << 17; /* group the tile's keys by length (the SORT pipeline) */
+[[maybe_unused]] constexpr int kVarWorkgroup = 1 << 16;
+[[maybe_unused]] constexpr int kVarRegStaged = 32;
+[[maybe_unused]] constexpr int kVarRingP5 = 128 | (3 << 8);
+[[maybe_unused]] constexpr int kVarRingP4 = 128;
+[[maybe_unused]] constexpr int kVarSorted = 1 << 17; /* group the tile's keys by length (the SORT pipeline) */
 constexpr int kVarOver = 1 << 18; /* workgroup pipelines: three resident sets of workgroups per launch */
 constexpr int kVarMd5Direct = 1 << 19; /* the direct per-lane block pipeline: md5 (nc_md5_kernels.hip) and
                                           the byte-serial modes (nc_bytes_kernels.hip); options in bits 20-23 */
-constexpr int kVarDirect = kVarMd5Direct;
+[[maybe_unused]] constexpr int kVarDirect = kVarMd5Direct;
 constexpr int kVarDirectLds = 4 << 20; /* its LDS-DMA block image (long keys) */
 constexpr int kVarDirectIl32 = (8 | 2) << 20; /* a wave's tiles interleaved over the grid, 32 per wave (nc_direct.h
                                                  wave_tiles) */

@@ -531,6 +531,73 @@ class Context:
         self._keep.pop(ticket, None)
 
 
+class Ring:
+    """nc_gpuhash_ring: small batches (one mbuf's keys) served by a resident
+    worker workgroup that polls mapped host memory — no HIP call per batch
+    (include/nc_gpuhash.h 3d)."""
+
+    def __init__(self, device: int = 0, nslots: int = 4, max_keys: int = 4095, max_key_bytes: int = 32768):
+        self._lib = L.lib()
+        handle = self._lib.nc_gpuhash_ring_create(device, nslots, max_keys, max_key_bytes)
+        if not handle:
+            raise L.NcError(ctypes.get_errno(), "nc_gpuhash_ring_create failed")
+        self._h = handle
+        self._keep: dict[int, tuple] = {}
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.nc_gpuhash_ring_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def launches(self) -> int:
+        """worker launches so far (the first submit's, and relaunches after idle)"""
+        return int(self._lib.nc_gpuhash_ring_launches(self._h))
+
+    def submit_spans(self, hash_: int | str, buf: np.ndarray, spans: Sequence[tuple[int, int]]) -> tuple[int, np.ndarray]:
+        """Spans are (start, end) byte offsets into `buf`; returns (ticket, out),
+        `out` valid once poll()/wait() says so."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        base = buf.ctypes.data
+        arr = (L.NcKeySpan * max(len(spans), 1))()
+        for i, (s, e) in enumerate(spans):
+            arr[i].start = base + s
+            arr[i].end = base + e
+        out = np.empty(len(spans), dtype=np.uint32)
+        ticket = ctypes.c_int(-1)
+        rc = self._lib.nc_gpuhash_ring_submit_spans(self._h, mode_of(hash_), arr, len(spans), out.ctypes.data,
+                                                    ctypes.byref(ticket))
+        if rc == L.NC_EAGAIN:
+            raise BlockingIOError("the next ring slot's batch is still in flight")
+        L.check(rc, "nc_gpuhash_ring_submit_spans")
+        self._keep[ticket.value] = (out,)
+        return ticket.value, out
+
+    def poll(self, ticket: int) -> bool:
+        rc = self._lib.nc_gpuhash_ring_poll(self._h, ticket)
+        if rc == L.NC_EAGAIN:
+            return False
+        L.check(rc, "nc_gpuhash_ring_poll")
+        self._keep.pop(ticket, None)
+        return True
+
+    def wait(self, ticket: int) -> None:
+        L.check(self._lib.nc_gpuhash_ring_wait(self._h, ticket), "nc_gpuhash_ring_wait")
+        self._keep.pop(ticket, None)
+
+
 class Pipe:
     """nc_gpuhash_pipe: whole host batches from caller-pinned memory, chunked
     H2D / kernel / D2H on three streams, no repacking (the large-batch host
