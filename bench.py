@@ -24,7 +24,7 @@ with HIP events on the launch stream:
   server_idx  fused hash -> ketama dispatch on the C2 keys (§8f.1);
   redis_key_extraction  2^20 pipelined RESP GETs parsed on the device (§8f.4);
   c5_e2e      the pipelined GET replay (configs[4]) through the host batch
-              API, PCIe-inclusive (tools/nc_c5_replay);
+              API and the batch ring, PCIe-inclusive (tools/nc_c5_replay);
   cpu_baseline  the reference hashkit compiled from /root/reference, timed on
               this host (rank 0, N = 1).
 """
@@ -669,8 +669,9 @@ def e2e_leg(t, torch, cfg, spec, first, n, mode, dev, digest_rank, world, rank, 
 
 def c5_leg(seconds=0.4):
     """tools/nc_c5_replay: 64 x 128 pipelined GETs read into 16,336-byte mbufs
-    with repair, one mbuf's keys per submit_spans batch, depth 1/2/4, copy and
-    zero-copy, next to the per-key host hash of the same spans."""
+    with repair, one mbuf's keys per batch: the context path (submit_spans,
+    depth 1/2/4, copy and zero-copy) and the batch ring (no HIP call per
+    batch, depth 1/2/4/8), next to the per-key host hash of the same spans."""
     exe = os.path.join(HERE, "tools", "nc_c5_replay")
     if not os.path.exists(exe):
         return {"error": "tools/nc_c5_replay not built"}
@@ -684,9 +685,11 @@ def c5_leg(seconds=0.4):
     host = [r for r in rows if r["point"] == "host_per_key"]
     gpu = [r for r in rows if r["point"] == "gpu"]
     return {"workload": "C5: 64 connections x 128 pipelined 'get <key>\\r\\n' (Zipf 8-64 B printable keys) read "
-                        "into 16,336-byte mbufs with repair; one mbuf's keys per nc_gpuhash_submit_spans batch; "
-                        "host->device->host, fnv1a_64",
+                        "into 16,336-byte mbufs with repair; one mbuf's keys per batch (nc_gpuhash_submit_spans "
+                        "or the batch ring); host->device->host, fnv1a_64",
             "host_per_key": host[0] if host else None, "gpu": gpu,
+            "ring_best_depth_ge2": max((r for r in gpu if r["path"].startswith("ring") and r["depth"] >= 2),
+                                       key=lambda r: r["mkeys_s"], default=None),
             "mismatches": int(sum(r["mismatches"] for r in gpu))}
 
 

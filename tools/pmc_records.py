@@ -16,7 +16,9 @@ WRITE_SIZE and the two SQ groups, one rocprofv3 run each) of the hash kernel
                      with tools/probes/md5_rate.hip: VOP3 ~4.2, VOP2 ~2.4)
   wait_any_over_wave_cycles = SQ_WAIT_ANY / SQ_WAVE_CYCLES
   lds_bank_conflict_cycles_per_cu = SQ_LDS_BANK_CONFLICT / 256
-The algorithmic bytes come from the bench line's legs (C2 keys + 12 B/key).
+  valu_lane_inst_over_alg_ops = 64 x SQ_INSTS_VALU / the leg's alg_ops_per_launch
+                     (md5: 324 lane-ops per 64-byte block)
+The algorithmic bytes (and md5 ops) come from the bench line's legs.
 """
 import json
 import os
@@ -69,17 +71,37 @@ def record(d, tag, alg):
     return out
 
 
+def leg_of(line, cfg, mode):
+    """the bench line's leg for CFG:MODE (C4S = the C4 shard)"""
+    if cfg == "C2":
+        return {"fnv1a_64": line, "md5": line.get("md5"), "server_idx": line.get("server_idx_ketama")}.get(mode)
+    if cfg == "C3":
+        return line.get(f"c3_{mode}")
+    if cfg in ("C4", "C4S"):
+        return line.get("c4_shard", {}).get(mode)
+    return None
+
+
+def roofs(leg):
+    return [leg[k] for k in ("roofline_hbm", "roofline", "roofline_valu") if isinstance(leg.get(k), dict)] if leg else []
+
+
 def main():
     d, bench = sys.argv[1], json.load(open(sys.argv[2]))
     line = bench.get("plain_run", bench)
-    c2_alg = line["roofline"]["alg_bytes_per_launch"]
     work = {}
     for spec in sys.argv[3:]:
         cfg, mode = spec.split(":")
-        alg = c2_alg if cfg == "C2" else None
+        rf = roofs(leg_of(line, cfg, mode))
+        alg = next((r["alg_bytes_per_launch"] for r in rf if "alg_bytes_per_launch" in r), None)
+        ops = next((r["alg_ops_per_launch"] for r in rf if "alg_ops_per_launch" in r), None)
         r = record(d, f"{cfg}_{mode}_0", alg)
         if r:
-            work.setdefault(cfg, {})[mode] = r
+            if ops and "SQ_INSTS_VALU" in r:
+                # md5: lane instructions issued (64 per wave instruction) over
+                # the algorithm's 324 per 64-byte block
+                r["valu_lane_inst_over_alg_ops"] = round(64 * r["SQ_INSTS_VALU"] / ops, 4)
+            work.setdefault("C4" if cfg == "C4S" else cfg, {})[mode] = r
     print(json.dumps({"note": "per launch of the hash kernel; " + __doc__.split("derives what DESIGN.md quotes:")[0]
                       .strip().splitlines()[0] + " (tools/pmc_records.py)", "source": d, "workloads": work}, indent=1))
 
