@@ -356,21 +356,15 @@ def test_wave_ring_ragged_tiles(gpu, oracle, var):
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
 
 
-BT = 1 << 28  # crcs on the direct pipeline: the byte table, one copy per LDS bank
-
-
 @pytest.mark.parametrize("var", [1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (8 << 20), (1 << 19) | (10 << 20),
-                                 (1 << 19) | (11 << 20), (1 << 19) | (14 << 20), (1 << 19) | (9 << 20),
-                                 (1 << 19) | (10 << 20) | BT, (1 << 19) | (14 << 20) | BT],
-                         ids=["direct", "lines", "il16", "il32", "il64", "lines_il32", "il8", "il32_bt",
-                              "lines_il32_bt"])
+                                 (1 << 19) | (11 << 20), (1 << 19) | (14 << 20), (1 << 19) | (9 << 20)],
+                         ids=["direct", "lines", "il16", "il32", "il64", "lines_il32", "il8"])
 def test_direct_ragged_tiles(gpu, oracle, var):
     """The direct per-lane pipelines (md5 and the byte-serial modes; the other
     modes take their default pipeline), consecutive or grid-interleaved tiles
-    per wave, crcs through slicing-by-4 or the per-bank byte table, on batch
-    sizes around the 64-key tile and the per-workgroup tile count, with empty
-    keys, one-block, multi-block and padding-only-block keys, a misaligned key
-    buffer, against the oracle."""
+    per wave, on batch sizes around the 64-key tile and the per-workgroup tile
+    count, with empty keys, one-block, multi-block and padding-only-block keys,
+    a misaligned key buffer, against the oracle."""
     L.lib().nc_gpuhash_set_tuning(0, 0, var)
     try:
         for n, spec in ((1, t.SynthSpec.uniform(40, 0, 3)), (63, t.SynthSpec.zipf(41)), (64, t.SynthSpec.fixed(42, 32)),

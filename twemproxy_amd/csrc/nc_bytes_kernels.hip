@@ -52,26 +52,16 @@ __device__ __forceinline__ uint32_t final_state(uint32_t h)
 }
 
 /* ---- crc tables: slicing-by-4 (nc_crc_slice.h), replicated over 8 bank
- * groups (R = 8, 32 KiB); or (BT) the byte table alone, one copy per bank
- * (R = 32, 32 KiB): a 32-lane group's lookups never conflict, at one
- * dependent lookup per byte ---- */
+ * groups (R = 8, 32 KiB) ---- */
 constexpr uint32_t kCopies = 8;
 constexpr uint32_t kTabWords = nc_slice::table_words<kCopies>();
-constexpr uint32_t kBtCopies = 32;
-static_assert(256u * kBtCopies == kTabWords, "both table forms fill the same 32 KiB");
-
-template <bool BT>
-constexpr uint32_t copies()
-{
-    return BT ? kBtCopies : kCopies;
-}
 
 /* byte j (0..3) of word w into state h (the crcs through T0) */
-template <int MODE, bool BT = false>
+template <int MODE>
 __device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t w, int j, const uint32_t *tab, uint32_t lane4)
 {
     const uint32_t b = (w >> (8 * j)) & 0xffu;
-    if constexpr (has_table<MODE>()) return nc_slice::byte<MODE, copies<BT>()>(h, b, tab, lane4);
+    if constexpr (has_table<MODE>()) return nc_slice::byte<MODE, kCopies>(h, b, tab, lane4);
     else if constexpr (MODE == NC_GPUHASH_FNV1A_64) return nc_fnv1a_64_step(h, b);
     else if constexpr (MODE == NC_GPUHASH_FNV1_64) return nc_fnv1_64_step(h, b);
     else if constexpr (MODE == NC_GPUHASH_FNV1_32) return nc_fnv1_32_step(h, b);
@@ -80,30 +70,30 @@ __device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t w, int j, con
 }
 
 /* the 4 bytes of word w */
-template <int MODE, bool BT>
+template <int MODE>
 __device__ __forceinline__ uint32_t word_step(uint32_t h, uint32_t w, const uint32_t *tab, uint32_t lc4)
 {
-    if constexpr (has_table<MODE>() && !BT) {
+    if constexpr (has_table<MODE>()) {
         return nc_slice::word<MODE, kCopies>(h, w, tab, lc4);
     } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++) h = byte_step<MODE, BT>(h, w, j, tab, lc4);
+        for (int j = 0; j < 4; j++) h = byte_step<MODE>(h, w, j, tab, lc4);
         return h;
     }
 }
 
 /* the first nb (1..4, per lane) bytes of word w, one at a time */
-template <int MODE, bool BT>
+template <int MODE>
 __device__ __forceinline__ uint32_t bytes_step(uint32_t h, uint32_t w, int32_t nb, const uint32_t *tab, uint32_t lc4)
 {
 #pragma unroll
     for (int j = 0; j < 4; j++)
-        if (j < nb) h = byte_step<MODE, BT>(h, w, j, tab, lc4);
+        if (j < nb) h = byte_step<MODE>(h, w, j, tab, lc4);
     return h;
 }
 
 /* nb (per lane, may exceed 64) key bytes of one block in d */
-template <int MODE, bool BT>
+template <int MODE>
 __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], int32_t nb, const uint32_t *tab,
                                                uint32_t lane4)
 {
@@ -113,9 +103,9 @@ __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], 
         const uint32_t w = d[t >> 2][t & 3];
         /* crc16 keeps its key's last 2+ bytes for the byte steps, which
          * rebuild the state's history bits (nc_crc_slice.h word) */
-        constexpr int32_t kWhole = BT ? 4 : nc_slice::whole<MODE>();
-        if (kb >= kWhole) h = word_step<MODE, BT>(h, w, tab, lane4);
-        else if (kb > 0) h = bytes_step<MODE, BT>(h, w, kb, tab, lane4);
+        constexpr int32_t kWhole = nc_slice::whole<MODE>();
+        if (kb >= kWhole) h = word_step<MODE>(h, w, tab, lane4);
+        else if (kb > 0) h = bytes_step<MODE>(h, w, kb, tab, lane4);
     }
     return h;
 }
@@ -128,7 +118,7 @@ __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], 
  * key that has one into its state; the next round's block is in flight (the
  * other register set, or the LDS image) while this one computes.
  */
-template <int MODE, bool LDS, bool IL, bool BT>
+template <int MODE, bool LDS, bool IL>
 __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__restrict__ keys,
                                                               const uint64_t *__restrict__ off, uint64_t nkeys,
                                                               uint32_t *__restrict__ out, uint64_t ntiles,
@@ -140,16 +130,12 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
     __shared__ uint32_t tab[has_table<MODE>() ? kTabWords : 1];
     __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kLineImage : 16];
     if constexpr (has_table<MODE>()) {
-        if constexpr (BT) {
-            for (uint32_t i = threadIdx.x; i < kTabWords; i += 1024u) tab[i] = nc_slice::entry<MODE>(0u, i / kBtCopies);
-        } else {
-            nc_slice::fill<MODE, kCopies>(tab, threadIdx.x, 1024u);
-        }
+        nc_slice::fill<MODE, kCopies>(tab, threadIdx.x, 1024u);
         __syncthreads();
     }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane4 = nc_slice::copy_of<copies<BT>()>(lane); /* this lane's table copy */
+    const uint32_t lane4 = nc_slice::copy_of<kCopies>(lane); /* this lane's table copy */
     const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
     uint32_t tile = 0; /* local tile index */
     const uint32_t tlast = tiles.n;
@@ -184,9 +170,9 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
 
         const int32_t rem = (int32_t)cur_t.len - (int32_t)RB * (int32_t)b;
         if (cur_t.valid && (rem > 0 || (b == 0u && cur_t.len == 0u))) {
-            h = block_step<MODE, BT>(h, cur, rem, tab, lane4);
+            h = block_step<MODE>(h, cur, rem, tab, lane4);
             if constexpr (LDS) {
-                if (rem > 64) h = block_step<MODE, BT>(h, nxt, rem - 64, tab, lane4);
+                if (rem > 64) h = block_step<MODE>(h, nxt, rem - 64, tab, lane4);
             }
             if (rem <= (int32_t)RB) {
                 const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
@@ -228,46 +214,26 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     (void)hipGetLastError();
     const bool il = (var & 8) != 0;
-    if constexpr (has_table<MODE>()) {
-        if (var & 16) { /* the byte table, one copy per bank */
-            if (var & 4) {
-                if (il)
-                    hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true, true>), dim3((unsigned)grid),
-                                       dim3(1024), 0, stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
-                else
-                    hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, false, true>), dim3((unsigned)grid),
-                                       dim3(1024), 0, stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
-            } else if (il) {
-                hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false, true, true>), dim3((unsigned)grid), dim3(1024),
-                                   0, stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
-            } else {
-                hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false, false, true>), dim3((unsigned)grid),
-                                   dim3(1024), 0, stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
-            }
-            return hipGetLastError();
-        }
-    }
     if (var & 4) {
         if (il)
-            hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true, false>), dim3((unsigned)grid), dim3(1024), 0,
-                               stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
+            hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true>), dim3((unsigned)grid), dim3(1024), 0, stream,
+                               d_keys, d_off, nkeys, d_out, ntiles, chunk);
         else
-            hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, false, false>), dim3((unsigned)grid), dim3(1024), 0,
-                               stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
+            hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, false>), dim3((unsigned)grid), dim3(1024), 0, stream,
+                               d_keys, d_off, nkeys, d_out, ntiles, chunk);
     } else if (il) {
-        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false, true, false>), dim3((unsigned)grid), dim3(1024), 0,
-                           stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
+        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false, true>), dim3((unsigned)grid), dim3(1024), 0, stream,
+                           d_keys, d_off, nkeys, d_out, ntiles, chunk);
     } else {
-        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false, false, false>), dim3((unsigned)grid), dim3(1024), 0,
-                           stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
+        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, false, false>), dim3((unsigned)grid), dim3(1024), 0, stream,
+                           d_keys, d_off, nkeys, d_out, ntiles, chunk);
     }
     return hipGetLastError();
 }
 
 /* the byte-serial modes on the direct pipeline; var: bits 0-1 tiles per wave
  * (16, 8, 32, 64), bit 2 the LDS-DMA block image (long keys), bit 3 a wave's
- * tiles interleaved over the grid (else consecutive), bit 4 (crcs) the byte
- * table with one copy per bank instead of slicing-by-4. nkeys < 2^32. */
+ * tiles interleaved over the grid (else consecutive). nkeys < 2^32. */
 bool supports(int mode)
 {
     switch (mode) {

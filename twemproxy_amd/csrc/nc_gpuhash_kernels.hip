@@ -2372,7 +2372,6 @@ constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline sta
 constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 4 sentinels), beside four 512-key
                                             workgroups per CU */
 constexpr int kVarNoPacked = 1 << 27; /* server_idx A/B: the 5-byte LDS continuum even where the packed one fits */
-constexpr int kVarCrcByteTable = 1 << 28; /* direct pipeline, crcs: the byte table, one copy per LDS bank */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2895,9 +2894,7 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
                                     : 0u;
             return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15, fl);
         }
-        if (nc_bytes::supports(mode))
-            return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream,
-                                    ((var >> 20) & 15) | ((var & kVarCrcByteTable) != 0 ? 16 : 0));
+        if (nc_bytes::supports(mode)) return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
     }
     if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))
         return nc_wsort::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
