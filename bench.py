@@ -688,8 +688,10 @@ def c5_leg(seconds=0.4):
                         "into 16,336-byte mbufs with repair; one mbuf's keys per batch (nc_gpuhash_submit_spans "
                         "or the batch ring); host->device->host, fnv1a_64",
             "host_per_key": host[0] if host else None, "gpu": gpu,
-            "ring_best_depth_ge2": max((r for r in gpu if r["path"].startswith("ring") and r["depth"] >= 2),
-                                       key=lambda r: r["mkeys_s"], default=None),
+            # the fastest ring point with >= 2 batches in flight and submit -> done <= 20 us
+            "ring_best_depth_ge2_le20us": max((r for r in gpu if r["path"].startswith("ring") and r["depth"] >= 2
+                                               and r["submit_to_done_us"] <= 20.0),
+                                              key=lambda r: r["mkeys_s"], default=None),
             "mismatches": int(sum(r["mismatches"] for r in gpu))}
 
 

@@ -349,7 +349,7 @@ def test_wave_ring_ragged_tiles(gpu, oracle, var):
         for n in (1, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 513, 1025, 4097):
             keys, off = t.synth_host(t.SynthSpec.zipf(60 + n % 7), 3, n)
             kd, od = to_dev(keys, off, shift=5)
-            for m in (1, 6, 3, 10):
+            for m in (1, 6, 3, 10, 2, 4):
                 np.testing.assert_array_equal(gpu_hash(m, kd, od), oracle.batch(m, keys, off),
                                               err_msg=f"var={var} n={n} mode={m}")
     finally:
