@@ -133,9 +133,9 @@ def test_batched_path_fails_loudly_without_gpu():
 def test_auto_policy_choices():
     """Shape-driven pipeline choice (host logic): md5 always on
     the direct per-lane block pipeline (its LDS-DMA line image from 64-byte
-    keys); the byte-serial modes on the direct pipeline for long keys and the
-    crcs for fixed short keys (tiles interleaved over the grid, 32 per wave,
-    for both); the register-staged workgroup pipeline when the
+    keys); the byte-serial modes on the direct pipeline for long keys (the
+    fnvs in eight-wave workgroups) and the crcs for fixed short keys (tiles
+    interleaved over the grid, 32 per wave, for both); the register-staged workgroup pipeline when the
     shape is unknown; oversubscribed workgroup grids (and length grouping) for
     varying lengths; the wave ring for fixed 20-40 B fnv-like keys; the
     grouped workgroup pipeline (one length quartile per wave) on C2-like
@@ -171,8 +171,10 @@ def test_auto_policy_choices():
     # short fixed, long keys (C4)
     assert t.pick_variant("fnv1a_64", n, (8 * n, 8, 8)) == WG
     assert t.pick_variant("md5", n, (16 * n, 16, 16)) == DIRECT
-    for name in ("crc32", "fnv1a_64", "one_at_a_time", "crc16", "fnv1_32"):
+    for name in ("crc32", "one_at_a_time", "crc16"):
         assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | IL32, name
+    for name in ("fnv1a_64", "fnv1_32"):  # eight-wave workgroups, one per CU
+        assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | IL32 | (1 << 27), name
     assert t.pick_variant("md5", n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS
     assert t.pick_variant("md5", n >> 3, (128 * (n >> 3), 128, 128)) == DIRECT | DIRECT_LDS
     assert t.pick_variant("murmur", n >> 3, (256 * (n >> 3), 256, 256)) == RING4

@@ -118,8 +118,8 @@ __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], 
  * key that has one into its state; the next round's block is in flight (the
  * other register set, or the LDS image) while this one computes.
  */
-template <int MODE, bool LDS, bool IL>
-__global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__restrict__ keys,
+template <int MODE, bool LDS, bool IL, int WAVES = kWaves>
+__global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8_t *__restrict__ keys,
                                                               const uint64_t *__restrict__ off, uint64_t nkeys,
                                                               uint32_t *__restrict__ out, uint64_t ntiles,
                                                               uint32_t chunk)
@@ -128,15 +128,15 @@ __global__ __launch_bounds__(1024) void nc_bytes_direct_kernel(const uint8_t *__
      * registers, or (LDS) one 128-byte line from the image */
     constexpr uint32_t RB = LDS ? 128u : 64u;
     __shared__ uint32_t tab[has_table<MODE>() ? kTabWords : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kLineImage : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? WAVES * kLineImage : 16];
     if constexpr (has_table<MODE>()) {
-        nc_slice::fill<MODE, kCopies>(tab, threadIdx.x, 1024u);
+        nc_slice::fill<MODE, kCopies>(tab, threadIdx.x, 64u * WAVES);
         __syncthreads();
     }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane4 = nc_slice::copy_of<kCopies>(lane); /* this lane's table copy */
-    const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
+    const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, WAVES, wave);
     uint32_t tile = 0; /* local tile index */
     const uint32_t tlast = tiles.n;
     if (tile >= tlast) return;
@@ -214,6 +214,19 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     (void)hipGetLastError();
     const bool il = (var & 8) != 0;
+    if ((var & 4) && (var & 16) && il) {
+        /* var bit 4: eight-wave workgroups, one per CU (unused dynamic LDS
+         * keeps a second out): half the concurrent key streams */
+        const uint64_t grid8 = (ntiles + 8u * chunk - 1u) / (8u * chunk);
+        if (grid8 > 0x7fffffffu) return hipErrorInvalidValue;
+        const uint32_t pad = has_table<MODE>() ? 0u : 40960u;
+        if (pad)
+            (void)hipFuncSetAttribute((const void *)nc_bytes_direct_kernel<MODE, true, true, 8>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad);
+        hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true, 8>), dim3((unsigned)grid8), dim3(512), pad, stream,
+                           d_keys, d_off, nkeys, d_out, ntiles, chunk);
+        return hipGetLastError();
+    }
     if (var & 4) {
         if (il)
             hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true>), dim3((unsigned)grid), dim3(1024), 0, stream,
@@ -233,7 +246,8 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
 
 /* the byte-serial modes on the direct pipeline; var: bits 0-1 tiles per wave
  * (16, 8, 32, 64), bit 2 the LDS-DMA block image (long keys), bit 3 a wave's
- * tiles interleaved over the grid (else consecutive). nkeys < 2^32. */
+ * tiles interleaved over the grid (else consecutive), bit 4 (with 2 and 3)
+ * eight-wave workgroups, one per CU. nkeys < 2^32. */
 bool supports(int mode)
 {
     switch (mode) {

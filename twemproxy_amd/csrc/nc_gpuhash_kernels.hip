@@ -2372,6 +2372,7 @@ constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline sta
 constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 4 sentinels), beside four 512-key
                                             workgroups per CU */
 constexpr int kVarNoPacked = 1 << 27; /* server_idx A/B: the 5-byte LDS continuum even where the packed one fits */
+constexpr int kVarDirect8 = 1 << 27; /* direct byte kernels, line image: eight-wave workgroups, one per CU */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2831,7 +2832,16 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
          * crc32 3.56 -> 2.24 ms, fnv1a_64 3.06 -> 2.15, one_at_a_time 3.22 ->
          * 2.48; 128-byte keys 0.79 -> 0.62 ms); the word modes keep the wave
          * ring, deeper or wider slab slots */
-        if (direct_bytes) return kVarDirect | kVarDirectLds | kVarDirectIl32; /* interleaved: C4 shard 1.92 -> 1.84 ms (crc32), 1.75 -> 1.66 (fnv1a_64) */
+        /* interleaved: C4 shard 1.92 -> 1.84 ms (crc32), 1.75 -> 1.66 (fnv1a_64);
+         * the fnvs at half the resident waves, 1.55 -> 1.52 (their streams
+         * contend for HBM; crc32's table lookups need the waves: 1.83 -> 2.22,
+         * profiles/r04_lines_occupancy_ab.jsonl) */
+        if (direct_bytes)
+            return kVarDirect | kVarDirectLds | kVarDirectIl32 |
+                   (mode == NC_GPUHASH_FNV1_64 || mode == NC_GPUHASH_FNV1A_64 || mode == NC_GPUHASH_FNV1_32 ||
+                            mode == NC_GPUHASH_FNV1A_32
+                        ? kVarDirect8
+                        : 0);
         if (mode == NC_GPUHASH_HSIEH) return kVarRingP5;
         return kVarRingP4;
     }
@@ -2894,7 +2904,9 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
                                     : 0u;
             return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15, fl);
         }
-        if (nc_bytes::supports(mode)) return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
+        if (nc_bytes::supports(mode))
+            return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream,
+                                    ((var >> 20) & 15) | ((var & kVarDirect8) != 0 ? 16 : 0));
     }
     if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))
         return nc_wsort::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
