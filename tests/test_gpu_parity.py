@@ -363,7 +363,8 @@ def test_wave_ring_ragged_tiles(gpu, oracle, var):
 def test_direct_ragged_tiles(gpu, oracle, var):
     """The direct per-lane pipelines (md5 and the byte-serial modes; the other
     modes take their default pipeline), consecutive or grid-interleaved tiles
-    per wave, on batch sizes around the 64-key tile and the per-workgroup tile
+    per wave, the byte modes' eight-wave line-image workgroups (bit 27), on
+    batch sizes around the 64-key tile and the per-workgroup tile
     count, with empty keys, one-block, multi-block and padding-only-block keys,
     a misaligned key buffer, against the oracle."""
     L.lib().nc_gpuhash_set_tuning(0, 0, var)
