@@ -358,9 +358,8 @@ def test_wave_ring_ragged_tiles(gpu, oracle, var):
 
 @pytest.mark.parametrize("var", [1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (8 << 20), (1 << 19) | (10 << 20),
                                  (1 << 19) | (11 << 20), (1 << 19) | (14 << 20), (1 << 19) | (9 << 20),
-                                 (1 << 19) | (14 << 20) | (1 << 27), (1 << 19) | (14 << 20) | (1 << 28)],
-                         ids=["direct", "lines", "il16", "il32", "il64", "lines_il32", "il8", "lines_il32_w8",
-                              "lines_il32_r16"])
+                                 (1 << 19) | (14 << 20) | (1 << 27)],
+                         ids=["direct", "lines", "il16", "il32", "il64", "lines_il32", "il8", "lines_il32_w8"])
 def test_direct_ragged_tiles(gpu, oracle, var):
     """The direct per-lane pipelines (md5 and the byte-serial modes; the other
     modes take their default pipeline), consecutive or grid-interleaved tiles

@@ -57,11 +57,11 @@ constexpr uint32_t kCopies = 8;
 constexpr uint32_t kTabWords = nc_slice::table_words<kCopies>();
 
 /* byte j (0..3) of word w into state h (the crcs through T0) */
-template <int MODE, uint32_t R = kCopies>
+template <int MODE>
 __device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t w, int j, const uint32_t *tab, uint32_t lane4)
 {
     const uint32_t b = (w >> (8 * j)) & 0xffu;
-    if constexpr (has_table<MODE>()) return nc_slice::byte<MODE, R>(h, b, tab, lane4);
+    if constexpr (has_table<MODE>()) return nc_slice::byte<MODE, kCopies>(h, b, tab, lane4);
     else if constexpr (MODE == NC_GPUHASH_FNV1A_64) return nc_fnv1a_64_step(h, b);
     else if constexpr (MODE == NC_GPUHASH_FNV1_64) return nc_fnv1_64_step(h, b);
     else if constexpr (MODE == NC_GPUHASH_FNV1_32) return nc_fnv1_32_step(h, b);
@@ -70,30 +70,30 @@ __device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t w, int j, con
 }
 
 /* the 4 bytes of word w */
-template <int MODE, uint32_t R>
+template <int MODE>
 __device__ __forceinline__ uint32_t word_step(uint32_t h, uint32_t w, const uint32_t *tab, uint32_t lc4)
 {
     if constexpr (has_table<MODE>()) {
-        return nc_slice::word<MODE, R>(h, w, tab, lc4);
+        return nc_slice::word<MODE, kCopies>(h, w, tab, lc4);
     } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++) h = byte_step<MODE, R>(h, w, j, tab, lc4);
+        for (int j = 0; j < 4; j++) h = byte_step<MODE>(h, w, j, tab, lc4);
         return h;
     }
 }
 
 /* the first nb (1..4, per lane) bytes of word w, one at a time */
-template <int MODE, uint32_t R>
+template <int MODE>
 __device__ __forceinline__ uint32_t bytes_step(uint32_t h, uint32_t w, int32_t nb, const uint32_t *tab, uint32_t lc4)
 {
 #pragma unroll
     for (int j = 0; j < 4; j++)
-        if (j < nb) h = byte_step<MODE, R>(h, w, j, tab, lc4);
+        if (j < nb) h = byte_step<MODE>(h, w, j, tab, lc4);
     return h;
 }
 
 /* nb (per lane, may exceed 64) key bytes of one block in d */
-template <int MODE, uint32_t R>
+template <int MODE>
 __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], int32_t nb, const uint32_t *tab,
                                                uint32_t lane4)
 {
@@ -104,8 +104,8 @@ __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], 
         /* crc16 keeps its key's last 2+ bytes for the byte steps, which
          * rebuild the state's history bits (nc_crc_slice.h word) */
         constexpr int32_t kWhole = nc_slice::whole<MODE>();
-        if (kb >= kWhole) h = word_step<MODE, R>(h, w, tab, lane4);
-        else if (kb > 0) h = bytes_step<MODE, R>(h, w, kb, tab, lane4);
+        if (kb >= kWhole) h = word_step<MODE>(h, w, tab, lane4);
+        else if (kb > 0) h = bytes_step<MODE>(h, w, kb, tab, lane4);
     }
     return h;
 }
@@ -118,7 +118,7 @@ __device__ __forceinline__ uint32_t block_step(uint32_t h, const u32x4 (&d)[4], 
  * key that has one into its state; the next round's block is in flight (the
  * other register set, or the LDS image) while this one computes.
  */
-template <int MODE, bool LDS, bool IL, int WAVES = kWaves, uint32_t R = kCopies>
+template <int MODE, bool LDS, bool IL, int WAVES = kWaves>
 __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8_t *__restrict__ keys,
                                                               const uint64_t *__restrict__ off, uint64_t nkeys,
                                                               uint32_t *__restrict__ out, uint64_t ntiles,
@@ -127,15 +127,15 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
     /* a round consumes RB bytes of every key: one 64-byte block from
      * registers, or (LDS) one 128-byte line from the image */
     constexpr uint32_t RB = LDS ? 128u : 64u;
-    __shared__ uint32_t tab[has_table<MODE>() ? nc_slice::table_words<R>() : 1];
+    __shared__ uint32_t tab[has_table<MODE>() ? kTabWords : 1];
     __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? WAVES * kLineImage : 16];
     if constexpr (has_table<MODE>()) {
-        nc_slice::fill<MODE, R>(tab, threadIdx.x, 64u * WAVES);
+        nc_slice::fill<MODE, kCopies>(tab, threadIdx.x, 64u * WAVES);
         __syncthreads();
     }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane4 = nc_slice::copy_of<R>(lane); /* this lane's table copy */
+    const uint32_t lane4 = nc_slice::copy_of<kCopies>(lane); /* this lane's table copy */
     const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, WAVES, wave);
     uint32_t tile = 0; /* local tile index */
     const uint32_t tlast = tiles.n;
@@ -170,9 +170,9 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
 
         const int32_t rem = (int32_t)cur_t.len - (int32_t)RB * (int32_t)b;
         if (cur_t.valid && (rem > 0 || (b == 0u && cur_t.len == 0u))) {
-            h = block_step<MODE, R>(h, cur, rem, tab, lane4);
+            h = block_step<MODE>(h, cur, rem, tab, lane4);
             if constexpr (LDS) {
-                if (rem > 64) h = block_step<MODE, R>(h, nxt, rem - 64, tab, lane4);
+                if (rem > 64) h = block_step<MODE>(h, nxt, rem - 64, tab, lane4);
             }
             if (rem <= (int32_t)RB) {
                 const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
@@ -214,18 +214,6 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     (void)hipGetLastError();
     const bool il = (var & 8) != 0;
-    if constexpr (has_table<MODE>()) {
-        if ((var & 4) && (var & 32) && il) {
-            /* A/B (var bit 5): twelve-wave workgroups with 16 table copies
-             * (96 KiB of line images + 64 KiB of tables, one per CU): half
-             * the lookups' bank conflicts at three quarters of the waves */
-            const uint64_t grid12 = (ntiles + 12u * chunk - 1u) / (12u * chunk);
-            if (grid12 > 0x7fffffffu) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true, 12, 16>), dim3((unsigned)grid12), dim3(768), 0,
-                               stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
-            return hipGetLastError();
-        }
-    }
     if ((var & 4) && (var & 16) && il) {
         /* var bit 4: eight-wave workgroups, one per CU (unused dynamic LDS
          * keeps a second out): half the concurrent key streams */

@@ -2373,7 +2373,6 @@ constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 4 sentinels)
                                             workgroups per CU */
 constexpr int kVarNoPacked = 1 << 27; /* server_idx A/B: the 5-byte LDS continuum even where the packed one fits */
 constexpr int kVarDirect8 = 1 << 27; /* direct byte kernels, line image: eight-wave workgroups, one per CU */
-constexpr int kVarDirectR16 = 1 << 28; /* A/B, crcs on the line image: twelve-wave workgroups, 16 table copies */
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2907,8 +2906,7 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
         }
         if (nc_bytes::supports(mode))
             return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream,
-                                    ((var >> 20) & 15) | ((var & kVarDirect8) != 0 ? 16 : 0) |
-                                        ((var & kVarDirectR16) != 0 ? 32 : 0));
+                                    ((var >> 20) & 15) | ((var & kVarDirect8) != 0 ? 16 : 0));
     }
     if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))
         return nc_wsort::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
