@@ -3,6 +3,7 @@ served by resident worker workgroups (one per lane) polling mapped host
 memory, no HIP call per batch. Every result against the oracle; the workers'
 life cycle (one launch per lane for a burst, leaving after an idle 10 ms and relaunching on demand,
 stopping on destroy) and the limits."""
+import threading
 import time
 
 import numpy as np
@@ -133,3 +134,40 @@ def test_ring_destroy_with_worker_running(gpu):
         r.submit_spans("fnv1a_64", buf, [(0, 10), (10, 200)])
         r.close()
     assert time.perf_counter() - t0 < 5.0
+
+
+def test_ring_shared_by_threads(gpu, oracle):
+    """four threads submit and wait on one ring (its mutex): every batch's
+    hashes are its own, none lost or delivered twice"""
+    errors = []
+    with t.Ring(0, nslots=4) as r:
+        def worker(seed):
+            rng = np.random.default_rng(seed)
+            try:
+                for _ in range(40):
+                    buf, spans = batch(rng, int(rng.integers(1, 400)), maxlen=48)
+                    while True:
+                        try:
+                            tk, out = r.submit_spans("fnv1a_64", buf, spans)
+                            break
+                        except BlockingIOError:
+                            time.sleep(0)
+                    r.wait(tk)
+                    np.testing.assert_array_equal(out, want(oracle, 6, buf, spans))
+            except Exception as e:  # reported by the main thread
+                errors.append(e)
+        th = [threading.Thread(target=worker, args=(40 + i,)) for i in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(60)
+        assert not any(x.is_alive() for x in th)
+    assert not errors, errors[0]
+
+
+def test_ring_rejects_spans_outside_the_buffer(gpu):
+    with t.Ring(0, nslots=2) as r:
+        buf = np.zeros(100, np.uint8)
+        for bad in ([(0, 101)], [(-1, 5)], [(10, 5)]):
+            with pytest.raises(ValueError):
+                r.submit_spans("fnv1a_64", buf, bad)

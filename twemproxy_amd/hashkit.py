@@ -505,6 +505,8 @@ class Context:
         base = buf.ctypes.data
         arr = (L.NcKeySpan * max(len(spans), 1))()
         for i, (s, e) in enumerate(spans):
+            if not 0 <= s <= e <= buf.size:  # the ring copies [s, e) out of buf before returning
+                raise ValueError(f"span {i} ({s}, {e}) is not inside the {buf.size}-byte buffer")
             arr[i].start = base + s
             arr[i].end = base + e
         out = np.empty(len(spans), dtype=np.uint32)
@@ -532,9 +534,11 @@ class Context:
 
 
 class Ring:
-    """nc_gpuhash_ring: small batches (one mbuf's keys) served by a resident
-    worker workgroup that polls mapped host memory — no HIP call per batch
-    (include/nc_gpuhash.h 3d)."""
+    """nc_gpuhash_ring: small batches (one mbuf's keys) served by resident
+    worker workgroups (one per lane, batch n on lane n % 2) that poll mapped
+    host memory — no HIP call per batch (include/nc_gpuhash.h 3d). Tickets
+    complete in order within a lane; poll each one. Thread-safe (the ring's
+    mutex)."""
 
     def __init__(self, device: int = 0, nslots: int = 4, max_keys: int = 4095, max_key_bytes: int = 32768):
         self._lib = L.lib()
@@ -573,6 +577,8 @@ class Ring:
         base = buf.ctypes.data
         arr = (L.NcKeySpan * max(len(spans), 1))()
         for i, (s, e) in enumerate(spans):
+            if not 0 <= s <= e <= buf.size:  # the ring copies [s, e) out of buf before returning
+                raise ValueError(f"span {i} ({s}, {e}) is not inside the {buf.size}-byte buffer")
             arr[i].start = base + s
             arr[i].end = base + e
         out = np.empty(len(spans), dtype=np.uint32)
