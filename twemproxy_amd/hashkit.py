@@ -505,7 +505,7 @@ class Context:
         base = buf.ctypes.data
         arr = (L.NcKeySpan * max(len(spans), 1))()
         for i, (s, e) in enumerate(spans):
-            if not 0 <= s <= e <= buf.size:  # the ring copies [s, e) out of buf before returning
+            if not 0 <= s <= e <= buf.size:  # [s, e) is copied out of buf before the call returns
                 raise ValueError(f"span {i} ({s}, {e}) is not inside the {buf.size}-byte buffer")
             arr[i].start = base + s
             arr[i].end = base + e
@@ -577,7 +577,7 @@ class Ring:
         base = buf.ctypes.data
         arr = (L.NcKeySpan * max(len(spans), 1))()
         for i, (s, e) in enumerate(spans):
-            if not 0 <= s <= e <= buf.size:  # the ring copies [s, e) out of buf before returning
+            if not 0 <= s <= e <= buf.size:  # [s, e) is copied out of buf before the call returns
                 raise ValueError(f"span {i} ({s}, {e}) is not inside the {buf.size}-byte buffer")
             arr[i].start = base + s
             arr[i].end = base + e
