@@ -38,7 +38,10 @@ def line():
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(HERE, "bench.py"), "--gpus", str(WORLD), "--steps", "3", "--warmup", "1",
            "--nkeys", str(NKEYS), "--c4-nkeys", str(C4_NKEYS), "--backend", "gloo", "--same-device"]
-    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    # 64 KiB scatter messages: the C4 shard's 1 MiB goes in 16 rounds, as
+    # an 8 GiB shard does in 1 GiB pieces on the 8-GPU node
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"),
+               NC_SCATTER_MAX_MSG_BYTES=str(1 << 16))
     p = subprocess.run(cmd, cwd=HERE, capture_output=True, text=True, timeout=400, env=env)
     assert p.returncode == 0, p.stderr[-4000:]
     rows = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

@@ -13,6 +13,8 @@ cuda:0, the one-GPU rehearsal of the multi-GPU bench).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -21,7 +23,7 @@ from ._lib import NC_GPUHASH_PAD
 # Largest single point-to-point message of the scatter: a C4 shard is 8 GiB;
 # it goes as 1 GiB pieces (one round per piece, see scatter_shards), so no
 # count or size inside the transport ever approaches 2^31 elements.
-MAX_MSG_BYTES = 1 << 30
+MAX_MSG_BYTES = int(os.environ.get("NC_SCATTER_MAX_MSG_BYTES", 1 << 30))  # smaller in the rehearsal tests
 
 
 def plan_bounds(offsets: torch.Tensor, nshards: int) -> torch.Tensor:
