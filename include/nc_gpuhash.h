@@ -312,7 +312,9 @@ rstatus_t nc_gpuhash_host_unregister(void *ptr);
  * worker is launched on its first batch, leaves after 10 ms of an empty ring
  * (or 2 s in any case) and is relaunched by the next submit or poll. Up to
  * nslots batches in flight, in order within a lane (the two lanes may finish
- * out of order: poll each ticket). Limits per batch:
+ * out of order: poll each ticket). A live worker holds one 1024-thread
+ * workgroup slot (one CU's worth of LDS for the batch image) while it polls,
+ * which batch kernels on the same GPU then run without. Limits per batch:
  * max_keys <= 4095 keys, max_key_bytes <= 32768 bytes (two mbufs' worth).
  * NULL with errno on failure (EINVAL limits, ENODEV no GPU). Thread-safe per
  * ring (one mutex). */
