@@ -175,8 +175,8 @@ def test_auto_policy_choices():
         assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | IL32, name
     for name in ("fnv1a_64", "fnv1_32"):  # eight-wave workgroups, one per CU
         assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | IL32 | (1 << 27), name
-    assert t.pick_variant("md5", n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS
-    assert t.pick_variant("md5", n >> 3, (128 * (n >> 3), 128, 128)) == DIRECT | DIRECT_LDS
+    assert t.pick_variant("md5", n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | (8 << 20)
+    assert t.pick_variant("md5", n >> 3, (128 * (n >> 3), 128, 128)) == DIRECT | DIRECT_LDS | (8 << 20)
     assert t.pick_variant("murmur", n >> 3, (256 * (n >> 3), 256, 256)) == RING4
     assert t.pick_variant("hsieh", 1000, (100000, 100, 100)) == RING5
     assert t.pick_variant("fnv1a_64", 0, (0, 0, 0)) == RS

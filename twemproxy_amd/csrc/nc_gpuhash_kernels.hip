@@ -2816,7 +2816,10 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
          * whose 64-byte pieces spare the texture addresser (C4 shard 3.1 ->
          * 2.1 ms, 128-byte keys 0.80 -> 0.62 ms; short keys are faster direct) */
         const bool lds = sh != nullptr && nkeys != 0 && sh->key_bytes / nkeys >= 64u;
-        return kVarMd5Direct | (lds ? (4 << 20) : 0);
+        /* ... with a wave's tiles interleaved over the grid (option bit 3):
+         * C4 shard 1.822-1.857 -> 1.803-1.830 ms in two same-box A/Bs
+         * (profiles/r04_lines_chunk_ab.jsonl, r04_crc_bytetable_ab.jsonl) */
+        return kVarMd5Direct | (lds ? (12 << 20) : 0);
     }
     if (sh == nullptr || nkeys == 0 || sh->key_bytes == 0) return kVarRegStaged;
     const uint64_t mean = sh->key_bytes / nkeys;
