@@ -2884,7 +2884,12 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
          * the previous tile's store: 0.464 -> 0.453 ms; fnv x4 / murmur lose
          * ~1 % that way (profiles/r03_c2_gs_ab.jsonl) */
         if (mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarGsort | kVarGsortCs | kVarGsort512 | kVarGsortIssue;
-        return kVarGsort | kVarGsortCs | kVarGsort512 | (2 << 21);
+        /* the fnvs at six resident sets, murmur at three: fnv1a_64 0.4186 ->
+         * 0.4119-0.4145 ms on one box, 0.4131 -> 0.4118 on another, fnv1_32
+         * 0.4129 -> 0.4111, murmur 0.4077 -> 0.4095
+         * (profiles/r04_c2_gs_sets_ab.jsonl) */
+        if (mode == NC_GPUHASH_MURMUR) return kVarGsort | kVarGsortCs | kVarGsort512 | (2 << 21);
+        return kVarGsort | kVarGsortCs | kVarGsort512;
     }
     if (crc || mode == NC_GPUHASH_ONE_AT_A_TIME) return kVarRegStaged | kVarOver;
     return kVarRegStaged;
