@@ -55,6 +55,7 @@ struct TileKeys {
     uint32_t srel; /* this lane's key start - s0 */
     uint32_t len;
     bool valid;
+    uint32_t nv; /* wave-uniform: the tile's keys below nkeys (valid = lane < nv) */
 };
 
 /* Offsets of a tile, as loaded (consumed one round later). */
@@ -148,8 +149,12 @@ struct Walker {
         t.len = o.e - o.s;
         /* the tile's key count, uniform and 32-bit (lane < it: one VALU compare) */
         const uint32_t k0 = key0(tl);
-        const uint32_t nv = k0 < nkeys ? nkeys - k0 : 0u;
+        /* on the scalar unit: hipcc turns the plain form into a saturating
+         * VALU subtract (and the tile selects that follow into v_cndmask) */
+        uint32_t nv;
+        asm("s_sub_u32 %0, %1, %2\n\ts_cselect_b32 %0, 0, %0" : "=&s"(nv) : "s"(nkeys), "s"(k0) : "scc");
         t.valid = lane < nv;
+        t.nv = nv;
         return t;
     }
 

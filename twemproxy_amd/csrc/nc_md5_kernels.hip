@@ -22,7 +22,9 @@
  *     key bytes: 0x80 or 0, zeros, and the bit length (nc_md5.c:263-274).
  *     Such lanes park their state in a per-wave LDS queue and the wave runs
  *     those tail blocks 64 at a time, so a Zipf tile with three 60-byte keys
- *     does not pay a second block for all 64 lanes;
+ *     does not pay a second block for all 64 lanes; a 56-64-byte key parks
+ *     after step 60 and its tail round runs steps 61-63 (run_tail), and the
+ *     workgroup pools its queues' leftovers at the end (flush_tails);
  *   - the final block of a key stops after step 60: the digest word returned
  *     is state A (nc_md5.c:317-320), and steps 61-63 only update B, C, D.
  *
@@ -49,7 +51,7 @@ using namespace nc_direct;
 
 /* per-wave LDS queue of keys waiting for their data-free last block */
 constexpr uint32_t kQ = 128;        /* entries per wave (>= 64 + 63) */
-constexpr uint32_t kQWords = 6;     /* A, B, C, D, length, key index */
+constexpr uint32_t kQWords = 9;     /* state X0..X3, length, key index, message words 11, 2, 9 */
 constexpr uint32_t kWaves = 4;      /* waves per workgroup */
 constexpr uint32_t kQBytes = kQ * kQWords * 4u;
 
@@ -64,23 +66,77 @@ __device__ __forceinline__ uint32_t lanemask_lt_popc(uint64_t m)
 }
 
 /* Tail blocks of up to 64 queued keys: message 0x80-or-0, zeros, bit length
- * (src/hashkit/nc_md5.c:263-274); out[index] = A + the block's A. */
+ * (src/hashkit/nc_md5.c:263-274); out[index] = A + the block's A. A key of
+ * 56..64 bytes (its one data block could not take the length) was queued
+ * after step 60 of that block: X is the working state then, and steps 61..63
+ * (message words 11, 2, 9) and the state add finish here, 64 lanes at a
+ * time, instead of in every round a wave holds such a key. Any other queued
+ * key (empty, or longer than 64 bytes) carries its chaining state in X. */
+__device__ __forceinline__ void tail_entry(const uint32_t *qw, uint32_t slot, uint32_t *__restrict__ out)
+{
+    uint32_t st[4] = {qw[0 * kQ + slot], qw[1 * kQ + slot], qw[2 * kQ + slot], qw[3 * kQ + slot]};
+    const uint32_t len = qw[4 * kQ + slot], idx = qw[5 * kQ + slot];
+    if (len - 56u <= 8u) {
+        uint32_t w[16];
+        w[11] = qw[6 * kQ + slot];
+        w[2] = qw[7 * kQ + slot];
+        w[9] = qw[8 * kQ + slot];
+        md5_steps_from61(st, w, std::make_integer_sequence<int, 3>{});
+        st[0] += NC_MD5_A0;
+        st[1] += NC_MD5_B0;
+        st[2] += NC_MD5_C0;
+        st[3] += NC_MD5_D0;
+    }
+    uint32_t w[16] = {};
+    w[0] = (len & 63u) == 0u ? 0x80u : 0u;
+    w[14] = len << 3;
+    w[15] = len >> 29;
+    /* words 1..13 are zero: folded into the steps' constants */
+    __builtin_nontemporal_store(md5_tail_final_a(st, w), out + idx);
+}
+
 __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__restrict__ out)
 {
     const uint32_t n = q.count < 64u ? q.count : 64u;
-    if (lane < n) {
-        const uint32_t slot = (q.head + lane) & (kQ - 1u);
-        const uint32_t st[4] = {q.w[0 * kQ + slot], q.w[1 * kQ + slot], q.w[2 * kQ + slot], q.w[3 * kQ + slot]};
-        const uint32_t len = q.w[4 * kQ + slot], idx = q.w[5 * kQ + slot];
-        uint32_t w[16] = {};
-        w[0] = (len & 63u) == 0u ? 0x80u : 0u;
-        w[14] = len << 3;
-        w[15] = len >> 29;
-        /* words 1..13 are zero: folded into the steps' constants */
-        __builtin_nontemporal_store(md5_tail_final_a(st, w), out + idx);
-    }
+    if (lane < n) tail_entry(q.w, (q.head + lane) & (kQ - 1u), out);
     q.head = (q.head + n) & (kQ - 1u);
     q.count -= n;
+}
+
+/* The workgroup's leftover queue entries at the end, pooled: batch k of 64
+ * from the concatenation of the waves' queues goes to wave k mod kWaves
+ * (one partly filled tail round per wave would cost each wave a full round
+ * of steps for its last few keys). Every wave of the workgroup calls it. */
+__device__ __forceinline__ void flush_tails(uint32_t *qmem, uint32_t (*qmeta)[2], const Queue &q, uint32_t wave,
+                                            uint32_t lane, uint32_t *__restrict__ out)
+{
+    if (lane == 0u) {
+        qmeta[wave][0] = q.head;
+        qmeta[wave][1] = q.count;
+    }
+    __syncthreads();
+    uint32_t head[kWaves], pre[kWaves + 1];
+    pre[0] = 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < kWaves; i++) {
+        head[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)qmeta[i][0]);
+        pre[i + 1] = pre[i] + (uint32_t)__builtin_amdgcn_readfirstlane((int)qmeta[i][1]);
+    }
+    for (uint32_t e0 = 64u * wave; e0 < pre[kWaves]; e0 += 64u * kWaves) {
+        const uint32_t e = e0 + lane;
+        if (e < pre[kWaves]) {
+            uint32_t sw = 0u;
+#pragma unroll
+            for (uint32_t i = 1; i < kWaves; i++) sw += e >= pre[i] ? 1u : 0u;
+            uint32_t h = head[0], p = pre[0];
+#pragma unroll
+            for (uint32_t i = 1; i < kWaves; i++) {
+                h = sw == i ? head[i] : h;
+                p = sw == i ? pre[i] : p;
+            }
+            tail_entry(qmem + sw * kQWords * kQ, (h + e - p) & (kQ - 1u), out);
+        }
+    }
 }
 
 } // namespace
@@ -98,6 +154,7 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                                                            uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
 {
     __shared__ uint32_t qmem[kWaves * kQWords * kQ];
+    __shared__ uint32_t qmeta[kWaves][2];
     /* LDS: the next round's blocks arrive by LDS-DMA into a per-wave 4 KiB
      * image (key k's 64 bytes at k * 64) instead of into registers */
     __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kImage : 16];
@@ -109,8 +166,8 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
     const Tiles<IL> tiles = wave_tiles<IL>(ntiles, chunk, kWaves, wave);
     uint32_t tile = 0; /* local tile index */
     const uint32_t tlast = tiles.n;
-    if (tile >= tlast) return;
     Queue q{qmem + wave * kQWords * kQ, 0u, 0u};
+    if (tile < tlast) { /* a wave without tiles still joins the workgroup's tail flush */
     Walker<IL> wk;
     wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + (LDS ? wave * kImage : 0u);
@@ -143,18 +200,18 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
      * out before the next round's loads could land there (24 v_mov per round
      * in the fixed-length form). */
     auto round = [&](u32x4 (&cur)[4], u32x4 (&nxt)[4]) __attribute__((always_inline)) {
-        const bool more = __ballot(cur_t.valid && cur_t.len > 64u * (b + 1u)) != 0ull;
+        const bool more = __ballot((lane < cur_t.nv) && cur_t.len > 64u * (b + 1u)) != 0ull;
         const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
         const int32_t rem = (int32_t)cur_t.len - 64 * (int32_t)b; /* key bytes from this block's start */
         const uint32_t len = cur_t.len;
-        const bool act = cur_t.valid && rem > 0;
+        const bool act = (lane < cur_t.nv) && rem > 0;
         if constexpr (LDS) wk.read_img(img, cur); /* this round's block, DMA'd during the previous round */
         /* FL: a tile whose keys all have FL bytes (checked: the shape only
          * picks the instantiation) takes its data words as loaded, the
          * boundary word by one constant perm, and constants for the rest.
          * Every form pads `cur` in place: the steps read it as it stands. */
         bool fl_tile = false;
-        if constexpr (FL > 0) fl_tile = __ballot(cur_t.valid && cur_t.len != (uint32_t)FL) == 0ull;
+        if constexpr (FL > 0) fl_tile = __ballot((lane < cur_t.nv) && cur_t.len != (uint32_t)FL) == 0ull;
         if (fl_tile) {
             if constexpr (FL > 0 && FL % 4 != 0) {
                 constexpr uint32_t bnd = FL % 4 == 1 ? kBoundary1 : (FL % 4 == 2 ? kBoundary2 : kBoundary3);
@@ -188,36 +245,46 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                     __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
                 }
             }
-        } else if (act) {
+        }
+        uint32_t v[4] = {st[0], st[1], st[2], st[3]}; /* a queued key's X (run_tail) */
+        if (!fl_tile && act) {
             const bool fin = rem <= 55;
             /* steps 0..60 for every lane; a key that ends here is done (A's
-             * last update is step 60), the others run steps 61..63 */
-            uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+             * last update is step 60); a key of 56..64 bytes leaves steps
+             * 61..63 to its tail block's round (run_tail); longer keys run
+             * them here */
             md5_steps(v, w, std::make_integer_sequence<int, 61>{});
             if (fin) {
                 const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
                 __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
-            } else {
+            } else if (len - 56u > 8u) {
                 md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
                 st[0] += v[0];
                 st[1] += v[1];
                 st[2] += v[2];
                 st[3] += v[3];
+                v[0] = st[0];
+                v[1] = st[1];
+                v[2] = st[2];
+                v[3] = st[3];
             }
         }
         /* keys whose last data block could not take the length (or empty
          * keys) queue their state for a data-free tail block */
-        const bool tail = cur_t.valid && ((rem <= 64 && rem >= 56) || (b == 0u && len == 0u));
+        const bool tail = (lane < cur_t.nv) && ((rem <= 64 && rem >= 56) || (b == 0u && len == 0u));
         const uint64_t tm = __ballot(tail);
         if (tm != 0ull) {
             if (tail) {
                 const uint32_t slot = (q.head + q.count + lanemask_lt_popc(tm)) & (kQ - 1u);
-                q.w[0 * kQ + slot] = st[0];
-                q.w[1 * kQ + slot] = st[1];
-                q.w[2 * kQ + slot] = st[2];
-                q.w[3 * kQ + slot] = st[3];
+                q.w[0 * kQ + slot] = v[0];
+                q.w[1 * kQ + slot] = v[1];
+                q.w[2 * kQ + slot] = v[2];
+                q.w[3 * kQ + slot] = v[3];
                 q.w[4 * kQ + slot] = len;
                 q.w[5 * kQ + slot] = wk.key0(tile) + lane;
+                q.w[6 * kQ + slot] = w[11];
+                q.w[7 * kQ + slot] = w[2];
+                q.w[8 * kQ + slot] = w[9];
             }
             q.count += (uint32_t)__builtin_popcountll(tm);
             if (q.count >= 64u) run_tail(q, lane, out);
@@ -242,7 +309,11 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
         round(db, da);
         if (tile >= tlast) break;
     }
-    while (q.count != 0u) run_tail(q, lane, out);
+    }
+    /* (pooled for the generic kernel; the fixed-length instantiations queue
+     * almost nothing, and the pooled flush there made hipcc spill) */
+    if constexpr (FL == 0) flush_tails(qmem, qmeta, q, wave, lane, out);
+    else while (q.count != 0u) run_tail(q, lane, out);
 }
 
 /*
