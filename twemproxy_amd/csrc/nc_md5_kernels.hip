@@ -246,48 +246,50 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                 }
             }
         }
-        uint32_t v[4] = {st[0], st[1], st[2], st[3]}; /* a queued key's X (run_tail) */
-        if (!fl_tile && act) {
-            const bool fin = rem <= 55;
-            /* steps 0..60 for every lane; a key that ends here is done (A's
-             * last update is step 60); a key of 56..64 bytes leaves steps
-             * 61..63 to its tail block's round (run_tail); longer keys run
-             * them here */
-            md5_steps(v, w, std::make_integer_sequence<int, 61>{});
-            if (fin) {
-                const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
-                __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
-            } else if (len - 56u > 8u) {
-                md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
-                st[0] += v[0];
-                st[1] += v[1];
-                st[2] += v[2];
-                st[3] += v[3];
-                v[0] = st[0];
-                v[1] = st[1];
-                v[2] = st[2];
-                v[3] = st[3];
+        if (!fl_tile) { /* (a fixed-length tile, FL <= 48, has no tail keys) */
+            uint32_t v[4] = {st[0], st[1], st[2], st[3]}; /* a queued key's X (run_tail) */
+            if (act) {
+                const bool fin = rem <= 55;
+                /* steps 0..60 for every lane; a key that ends here is done (A's
+                 * last update is step 60); a key of 56..64 bytes leaves steps
+                 * 61..63 to its tail block's round (run_tail); longer keys run
+                 * them here */
+                md5_steps(v, w, std::make_integer_sequence<int, 61>{});
+                if (fin) {
+                    const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
+                    __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
+                } else if (len - 56u > 8u) {
+                    md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
+                    st[0] += v[0];
+                    st[1] += v[1];
+                    st[2] += v[2];
+                    st[3] += v[3];
+                    v[0] = st[0];
+                    v[1] = st[1];
+                    v[2] = st[2];
+                    v[3] = st[3];
+                }
             }
-        }
-        /* keys whose last data block could not take the length (or empty
-         * keys) queue their state for a data-free tail block */
-        const bool tail = (lane < cur_t.nv) && ((rem <= 64 && rem >= 56) || (b == 0u && len == 0u));
-        const uint64_t tm = __ballot(tail);
-        if (tm != 0ull) {
-            if (tail) {
-                const uint32_t slot = (q.head + q.count + lanemask_lt_popc(tm)) & (kQ - 1u);
-                q.w[0 * kQ + slot] = v[0];
-                q.w[1 * kQ + slot] = v[1];
-                q.w[2 * kQ + slot] = v[2];
-                q.w[3 * kQ + slot] = v[3];
-                q.w[4 * kQ + slot] = len;
-                q.w[5 * kQ + slot] = wk.key0(tile) + lane;
-                q.w[6 * kQ + slot] = w[11];
-                q.w[7 * kQ + slot] = w[2];
-                q.w[8 * kQ + slot] = w[9];
+            /* keys whose last data block could not take the length (or empty
+             * keys) queue their state for a data-free tail block */
+            const bool tail = (lane < cur_t.nv) && ((rem <= 64 && rem >= 56) || (b == 0u && len == 0u));
+            const uint64_t tm = __ballot(tail);
+            if (tm != 0ull) {
+                if (tail) {
+                    const uint32_t slot = (q.head + q.count + lanemask_lt_popc(tm)) & (kQ - 1u);
+                    q.w[0 * kQ + slot] = v[0];
+                    q.w[1 * kQ + slot] = v[1];
+                    q.w[2 * kQ + slot] = v[2];
+                    q.w[3 * kQ + slot] = v[3];
+                    q.w[4 * kQ + slot] = len;
+                    q.w[5 * kQ + slot] = wk.key0(tile) + lane;
+                    q.w[6 * kQ + slot] = w[11];
+                    q.w[7 * kQ + slot] = w[2];
+                    q.w[8 * kQ + slot] = w[9];
+                }
+                q.count += (uint32_t)__builtin_popcountll(tm);
+                if (q.count >= 64u) run_tail(q, lane, out);
             }
-            q.count += (uint32_t)__builtin_popcountll(tm);
-            if (q.count >= 64u) run_tail(q, lane, out);
         }
 
         /* advance */
