@@ -303,34 +303,48 @@ rstatus_t nc_gpuhash_host_unregister(void *ptr);
 /* ---- 3d. small batches with no HIP call per batch: the batch ring ----
  * One mbuf's keys at a time (the batch site of src/nc_message.c:700-714 and
  * the fragment loops) without a kernel launch or an event per batch: the
- * ring's slots live in mapped, coherent host memory and resident worker
- * workgroups on the GPU poll them (csrc/nc_ring.hip): batch n belongs to lane
- * n % 2 (one lane when nslots == 1), each lane with its own worker. A submit
- * copies the spans' bytes into the slot (the mbufs may be recycled on return)
- * and publishes it with one store; the worker hashes it and writes the hashes
- * and a completion word back to host memory; poll is one load. A lane's
- * worker is launched on its first batch, leaves after 10 ms of an empty ring
- * (or 2 s in any case) and is relaunched by the next submit or poll. Up to
- * nslots batches in flight, in order within a lane (the two lanes may finish
- * out of order: poll each ticket). A live worker holds one 1024-thread
- * workgroup slot (one CU's worth of LDS for the batch image) while it polls,
- * which batch kernels on the same GPU then run without. Limits per batch:
- * max_keys <= 4095 keys, max_key_bytes <= 32768 bytes (two mbufs' worth).
- * NULL with errno on failure (EINVAL limits, ENODEV no GPU). Thread-safe per
- * ring (one mutex). */
+ * ring's slots live in mapped, coherent host memory and ONE resident launch
+ * polls them (csrc/nc_ring.hip), one workgroup per lane: batch n belongs to
+ * lane n % nlanes, each lane takes its batches in order, and the lanes'
+ * PCIe round trips overlap. A submit copies the spans' bytes into the slot
+ * (the mbufs may be recycled on return) and publishes it with one store; the
+ * lane's worker hashes it and writes the hashes and a completion word back
+ * to host memory; poll is one load. The launch starts on the first batch,
+ * ends after 10 ms with no batch on any lane or after 2 s (checked before
+ * every batch, under load too), and is relaunched by the next submit or
+ * poll: a batch published while the launch ends is served on a later poll,
+ * so poll (or wait) every ticket. Up to nslots batches in flight; lanes may
+ * finish out of order. A live launch holds nlanes workgroup slots (one lane's
+ * LDS holds its batch image) while it polls, which batch kernels on the same
+ * GPU then run without. Limits per batch: max_keys <= 4095 keys,
+ * max_key_bytes <= 32768 bytes (two mbufs' worth). NULL with errno on failure
+ * (EINVAL limits, ENODEV no GPU). Thread-safe per ring (one mutex). */
+#define NC_GPUHASH_RING_MAX_LANES 8
+#define NC_GPUHASH_RING_DEFAULT_LANES 8    /* capped at nslots */
+#define NC_GPUHASH_RING_DEFAULT_THREADS 1024
 typedef struct nc_gpuhash_ring nc_gpuhash_ring_t;
+/* nlanes = min(NC_GPUHASH_RING_DEFAULT_LANES, nslots) */
 nc_gpuhash_ring_t *nc_gpuhash_ring_create(int device, uint32_t nslots, uint32_t max_keys, uint64_t max_key_bytes);
+/* nlanes 1..NC_GPUHASH_RING_MAX_LANES (capped at nslots; 0 = default);
+ * threads per lane's workgroup 256, 512 or 1024 (0 = default) */
+nc_gpuhash_ring_t *nc_gpuhash_ring_create_ex(int device, uint32_t nslots, uint32_t max_keys, uint64_t max_key_bytes,
+                                             uint32_t nlanes, uint32_t threads);
 /* stops the workers (they return at their next poll) and frees the ring */
 void nc_gpuhash_ring_destroy(nc_gpuhash_ring_t *r);
 /* submit keypos-style spans; NC_EAGAIN when the next slot's batch is still in
- * flight, NC_ENOMEM past the limits; *ticket identifies the batch */
+ * flight, NC_ENOMEM past the limits, NC_ERROR/EINVAL for a NULL or inverted
+ * span (end < start); *ticket (0 .. 2^31-1) identifies the batch among the
+ * last 2^31 submitted */
 rstatus_t nc_gpuhash_ring_submit_spans(nc_gpuhash_ring_t *r, int mode, const struct nc_keyspan *spans,
                                        uint32_t nkeys, uint32_t *out, int *ticket);
-/* NC_OK once the batch's hashes are in its `out`, NC_EAGAIN before */
+/* NC_OK once the batch's hashes are in its `out`, NC_EAGAIN before, and
+ * NC_ERROR/EINVAL for a ticket this ring never issued */
 rstatus_t nc_gpuhash_ring_poll(nc_gpuhash_ring_t *r, int ticket);
 rstatus_t nc_gpuhash_ring_wait(nc_gpuhash_ring_t *r, int ticket);
-/* worker launches so far (the first submit's, and relaunches after idle) */
+/* launches so far (the first submit's, and relaunches after idle or 2 s) */
 uint64_t nc_gpuhash_ring_launches(const nc_gpuhash_ring_t *r);
+/* the ring's lane count */
+uint32_t nc_gpuhash_ring_lanes(const nc_gpuhash_ring_t *r);
 
 /* ---- 4. multi-GPU shard planning ----
  * Split keys [0, nkeys) into nshards contiguous ranges with about equal key

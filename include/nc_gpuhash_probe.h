@@ -79,6 +79,21 @@ rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const u
  * without its fixed-length specialisation (A/B); -1 = keep). */
 rstatus_t nc_gpuhash_set_tuning(int grid_cap, int sort, int variant);
 
+/* Batch ring diagnostics (tests only). start_seq: number the ring's batches
+ * from `seq` (a ring that has run for that long; EBUSY after the first
+ * submit). hold: 1 = launch no worker until set back to 0 (a submitted batch
+ * stays pending, so a poll must say NC_EAGAIN). */
+rstatus_t nc_gpuhash_ring_debug_start_seq(nc_gpuhash_ring_t *r, uint64_t seq);
+rstatus_t nc_gpuhash_ring_debug_hold(nc_gpuhash_ring_t *r, int hold);
+/* timeline: on = 1 before the first submit makes every batch record its
+ * device timeline in its slot (s_memrealtime, 100 MHz): [0] descriptor
+ * found, [1] batch staged in LDS, [2] every hash store issued, [3] stores
+ * acknowledged, written before the done word; [4] done word stored and [5]
+ * the lane's batch count, which reach host memory with the NEXT batch's
+ * release. on = -1 only reads slot `slot`'s eight words into out (when out is
+ * not NULL). */
+rstatus_t nc_gpuhash_ring_debug_timeline(nc_gpuhash_ring_t *r, int on, uint32_t slot, uint64_t out[8]);
+
 #ifdef __cplusplus
 }
 #endif

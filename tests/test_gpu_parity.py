@@ -356,14 +356,41 @@ def test_wave_ring_ragged_tiles(gpu, oracle, var):
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
 
 
+@pytest.mark.parametrize("var", [128 | 2048, 128 | 2048 | (1 << 12), 128 | 2048 | (2 << 12), 128 | 2048 | (3 << 12)],
+                         ids=["p5x7", "p5x6", "p5x4", "p4x8"])
+def test_wave_ring_crc_sliced(gpu, oracle, var):
+    """crc16 / crc32 / crc32a on the wave ring with slicing-by-16 tables shared
+    by the workgroup's waves (variant bit 11, bits 12-13 the ring), on ragged
+    batch sizes, fixed 32-byte keys (C3's shape), Zipf and uniform lengths
+    (every tail length; tiles too long for a slab slot take the global-memory
+    reader), misaligned key buffers, against the oracle."""
+    L.lib().nc_gpuhash_set_tuning(0, 0, var)
+    try:
+        for n, spec in ((1, t.SynthSpec.uniform(70, 0, 40)), (129, t.SynthSpec.fixed(71, 32)),
+                        (4097, t.SynthSpec.fixed(72, 32)), (1025, t.SynthSpec.zipf(73)),
+                        (3000, t.SynthSpec.uniform(74, 0, 40)), (2000, t.SynthSpec.uniform(75, 0, 300)),
+                        (777, t.SynthSpec.fixed(76, 17)), (513, t.SynthSpec.fixed(77, 2))):
+            keys, off = t.synth_host(spec, 3, n)
+            for shift in (0, 9):
+                kd, od = to_dev(keys, off, shift=shift)
+                for m in (2, 3, 4):
+                    np.testing.assert_array_equal(gpu_hash(m, kd, od), oracle.batch(m, keys, off),
+                                                  err_msg=f"var={var} n={n} spec={spec} mode={m} shift={shift}")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
 @pytest.mark.parametrize("var", [1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (8 << 20), (1 << 19) | (10 << 20),
                                  (1 << 19) | (11 << 20), (1 << 19) | (14 << 20), (1 << 19) | (9 << 20),
-                                 (1 << 19) | (14 << 20) | (1 << 27)],
-                         ids=["direct", "lines", "il16", "il32", "il64", "lines_il32", "il8", "lines_il32_w8"])
+                                 (1 << 19) | (14 << 20) | (1 << 12), (1 << 19) | (10 << 20) | (1 << 13),
+                                 (1 << 19) | (14 << 20) | (1 << 13), (1 << 19) | (1 << 13)],
+                         ids=["direct", "lines", "il16", "il32", "il64", "lines_il32", "il8", "lines_il32_w8",
+                              "il32_s8", "lines_il32_s8", "direct_s8"])
 def test_direct_ragged_tiles(gpu, oracle, var):
     """The direct per-lane pipelines (md5 and the byte-serial modes; the other
     modes take their default pipeline), consecutive or grid-interleaved tiles
-    per wave, the byte modes' eight-wave line-image workgroups (bit 27), on
+    per wave, the byte modes' eight-wave line-image workgroups (bit 12), the
+    crcs' slicing-by-8 tables (bit 13), on
     batch sizes around the 64-key tile and the per-workgroup tile
     count, with empty keys, one-block, multi-block and padding-only-block keys,
     a misaligned key buffer, against the oracle."""

@@ -1,8 +1,10 @@
 """The batch ring (nc_gpuhash_ring, include/nc_gpuhash.h 3d): small batches
-served by resident worker workgroups (one per lane) polling mapped host
-memory, no HIP call per batch. Every result against the oracle; the workers'
-life cycle (one launch per lane for a burst, leaving after an idle 10 ms and relaunching on demand,
-stopping on destroy) and the limits."""
+served by one resident launch (a workgroup per lane) polling mapped host
+memory, no HIP call per batch. Every result against the oracle; the launch's
+life cycle (one launch for a burst, ending after an idle 10 ms or 2 s and
+relaunching on demand, stopping on destroy), the lane and thread shapes, the
+ticket space across 2^31 and 2^32 batches, and the limits."""
+import ctypes
 import threading
 import time
 
@@ -36,14 +38,23 @@ def want(oracle, mode, buf, spans):
 
 def test_ring_every_mode_matches_oracle(gpu, oracle):
     rng = np.random.default_rng(31)
+    # batches and expected hashes first: the burst below has no host gap
+    # near the 10 ms idle limit
+    work = []
+    for m in range(12):
+        for nk in (1, 7, 64, 585, 1500):
+            buf, spans = batch(rng, nk)
+            work.append((m, nk, buf, spans, want(oracle, m, buf, spans)))
     with t.Ring(0, nslots=4) as r:
-        for m in range(12):
-            for nk in (1, 7, 64, 585, 1500):
-                buf, spans = batch(rng, nk)
-                tk, out = r.submit_spans(m, buf, spans)
-                r.wait(tk)
-                np.testing.assert_array_equal(out, want(oracle, m, buf, spans), err_msg=f"{t.HASH_NAMES[m]} {nk}")
-        assert r.launches == 2  # one worker per lane served the whole burst
+        outs = []
+        for m, nk, buf, spans, _ in work:
+            tk, out = r.submit_spans(m, buf, spans)
+            r.wait(tk)
+            outs.append(out)
+        launches = r.launches
+    for (m, nk, _, _, w), out in zip(work, outs):
+        np.testing.assert_array_equal(out, w, err_msg=f"{t.HASH_NAMES[m]} {nk}")
+    assert launches == 1  # one launch (a workgroup per lane) served the whole burst
 
 
 def test_ring_single_slot_single_lane(gpu, oracle):
@@ -171,3 +182,142 @@ def test_ring_rejects_spans_outside_the_buffer(gpu):
         for bad in ([(0, 101)], [(-1, 5)], [(10, 5)]):
             with pytest.raises(ValueError):
                 r.submit_spans("fnv1a_64", buf, bad)
+
+
+@pytest.mark.parametrize("lanes,threads", [(1, 256), (2, 512), (3, 1024), (4, 256), (8, 256), (8, 1024)])
+def test_ring_lane_shapes(gpu, oracle, lanes, threads):
+    """every lane count and workgroup size, batches pipelined over 8 slots"""
+    rng = np.random.default_rng(50 + lanes * 7 + threads)
+    work = []
+    for i in range(80):
+        buf, spans = batch(rng, int(rng.integers(0, 1200)), maxlen=70)
+        work.append((i % 12, buf, spans, want(oracle, i % 12, buf, spans)))
+    done = []
+    with t.Ring(0, nslots=8, lanes=lanes, threads=threads) as r:
+        assert r.lanes == lanes
+        pending = []
+        for m, buf, spans, w in work:
+            while True:
+                try:
+                    tk, out = r.submit_spans(m, buf, spans)
+                    break
+                except BlockingIOError:
+                    tk0, out0, w0 = pending.pop(0)
+                    r.wait(tk0)
+                    done.append((out0, w0))
+            pending.append((tk, out, w))
+        for tk, out, w in pending:
+            r.wait(tk)
+            done.append((out, w))
+        launches = r.launches
+    assert len(done) == len(work)
+    for out, w in done:
+        np.testing.assert_array_equal(out, w)
+    assert launches == 1
+
+
+@pytest.mark.parametrize("start", [2**31 - 21, 2**32 - 23, 2**33 + 5])
+@pytest.mark.parametrize("nslots", [3, 4])
+def test_ring_ticket_wrap(gpu, oracle, start, nslots):
+    """a ring that has already numbered `start` batches: across 2^31 (the
+    ticket's 31 bits wrap) and 2^32 (a 32-bit count would wrap), with slot
+    counts that do (4) and do not (3) divide 2^32, every batch's hashes are
+    its own, a delivered ticket polls done, and an unissued ticket is an
+    error, never NC_OK"""
+    rng = np.random.default_rng(start % 1000 + nslots)
+    with t.Ring(0, nslots=nslots) as r:
+        r.debug_start_seq(start)
+        with pytest.raises(t.NcError):
+            r.poll(start & 0x7FFFFFFF)  # not issued yet
+        pending, tickets = [], []
+        for i in range(60):
+            m = (i * 5) % 12
+            buf, spans = batch(rng, int(rng.integers(1, 400)), maxlen=40)
+            while True:
+                try:
+                    tk, out = r.submit_spans(m, buf, spans)
+                    break
+                except BlockingIOError:
+                    tk0, out0, b0, s0, m0 = pending.pop(0)
+                    r.wait(tk0)
+                    np.testing.assert_array_equal(out0, want(oracle, m0, b0, s0))
+            assert tk == (start + i) & 0x7FFFFFFF
+            tickets.append(tk)
+            pending.append((tk, out, buf, spans, m))
+        for tk, out, buf, spans, m in pending:
+            r.wait(tk)
+            np.testing.assert_array_equal(out, want(oracle, m, buf, spans))
+        for tk in tickets:  # all delivered, the oldest through their slots' reuse
+            assert r.poll(tk)
+        with pytest.raises(t.NcError):
+            r.poll((start + 60) & 0x7FFFFFFF)  # the next ticket: not issued
+        with pytest.raises(t.NcError):
+            r.poll((start - 1) & 0x7FFFFFFF)  # before the ring's first batch
+        with pytest.raises(t.NcError):
+            r.debug_start_seq(0)  # only a fresh ring
+
+
+def test_ring_pending_batch_never_polls_done(gpu, oracle):
+    """while no worker runs (debug hold), a submitted batch polls NC_EAGAIN
+    every time; released, the same ticket completes with its own hashes"""
+    rng = np.random.default_rng(61)
+    with t.Ring(0, nslots=3) as r:
+        r.debug_hold(True)
+        items = []
+        for m in (6, 1, 3):
+            buf, spans = batch(rng, 200, maxlen=50)
+            tk, out = r.submit_spans(m, buf, spans)
+            items.append((tk, out, buf, spans, m))
+        t_end = time.perf_counter() + 0.05
+        while time.perf_counter() < t_end:
+            for tk, *_ in items:
+                assert not r.poll(tk)
+        with pytest.raises(BlockingIOError):
+            r.submit_spans(6, *batch(rng, 10))  # every slot pending
+        assert r.launches == 0
+        r.debug_hold(False)
+        for tk, out, buf, spans, m in items:
+            r.wait(tk)
+            np.testing.assert_array_equal(out, want(oracle, m, buf, spans))
+        assert r.launches == 1
+
+
+def test_ring_relaunch_under_steady_load(gpu, oracle):
+    """a launch lives at most 2 s even while batches keep coming: it ends and
+    the next submit or poll relaunches it, with no batch lost"""
+    rng = np.random.default_rng(62)
+    bufs = [batch(rng, 300, maxlen=40) for _ in range(8)]
+    wants = [want(oracle, 6, b, s) for b, s in bufs]
+    with t.Ring(0, nslots=4) as r:
+        t_end = time.perf_counter() + 2.6
+        i = 0
+        while time.perf_counter() < t_end:
+            buf, spans = bufs[i % 8]
+            tk, out = r.submit_spans("fnv1a_64", buf, spans)
+            r.wait(tk)
+            np.testing.assert_array_equal(out, wants[i % 8])
+            i += 1
+        assert r.launches >= 2, (r.launches, i)
+
+
+def test_ring_c_rejects_inverted_and_null_spans(gpu, oracle):
+    """the C entry point itself (below the Python checks): a span with end <
+    start, or a NULL start, is EINVAL before anything is staged; the ring
+    then serves the next batch normally"""
+    lib = t._lib.lib()
+    buf = (ctypes.c_uint8 * 256)(*range(256))
+    base = ctypes.addressof(buf)
+    with t.Ring(0, nslots=2) as r:
+        out = (ctypes.c_uint32 * 4)()
+        tk = ctypes.c_int(-1)
+        for bad in ([(base + 10, base + 5)], [(base, base + 4), (base + 100, base + 99)], [(0, 8)]):
+            spans = (t._lib.NcKeySpan * len(bad))()
+            for i, (s0, e0) in enumerate(bad):
+                spans[i].start = s0
+                spans[i].end = e0
+            rc = lib.nc_gpuhash_ring_submit_spans(r._h, 6, spans, len(bad), ctypes.addressof(out), ctypes.byref(tk))
+            assert rc == t._lib.NC_ERROR and ctypes.get_errno() == 22, (bad, rc)
+        tk2, out2 = r.submit_spans("fnv1a_64", np.frombuffer(bytes(buf), np.uint8), [(0, 10), (10, 40)])
+        r.wait(tk2)
+        assert tk2 == 0  # the refused submits took no ticket
+        assert out2.tolist() == [t.hash_key("fnv1a_64", bytes(range(10))), t.hash_key("fnv1a_64", bytes(range(10, 40)))]

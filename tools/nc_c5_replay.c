@@ -13,7 +13,7 @@
  * way the fragment loop would.
  *
  * For in-flight depths 1, 2 and 4 (context slots), copy and zero-copy paths,
- * and depths 1, 2, 4 and 8 of the batch ring (nc_gpuhash_ring: a resident
+ * and depths 1, 2, 4, 8 and 16 of the batch ring (nc_gpuhash_ring: a resident
  * worker polls mapped host memory, no HIP call per batch),
  * it reports submit->done latency per mbuf and keys/s, and beside them the
  * per-key host hash of the same spans through a hash_t pointer (one core, as
@@ -21,6 +21,8 @@
  * checked against that host hash.
  *
  *   tools/nc_c5_replay [seconds-per-point]        (one JSON line per point)
+ *   tools/nc_c5_replay SECONDS timeline           (the ring at one batch in
+ *       flight with its device timeline: where a batch's submit -> done goes)
  */
 #define _GNU_SOURCE
 #include <inttypes.h>
@@ -30,6 +32,7 @@
 #include <time.h>
 
 #include "nc_gpuhash.h"
+#include "nc_gpuhash_probe.h"
 #include "nc_gpuhash_synth.h"
 
 #define NCONN 64
@@ -51,6 +54,81 @@ struct mbuf {
 };
 
 typedef uint32_t (*hash_t)(const char *, size_t);
+
+static uint32_t *first_of(const struct mbuf *mb, uint32_t nmb)
+{
+    uint32_t *first = malloc((nmb + 1) * sizeof(uint32_t));
+    if (!first) exit(1);
+    first[0] = 0;
+    for (uint32_t i = 0; i < nmb; i++) first[i + 1] = first[i] + mb[i].nkeys;
+    return first;
+}
+
+static int cmp_d(const void *a, const void *b)
+{
+    const double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* one batch in flight through the batch ring, with the worker's timeline:
+ * host submit call; device found -> staged (the batch fetched across PCIe
+ * into LDS) -> issued (hashes computed, stores issued) -> stored (stores
+ * acknowledged) -> released (done word stored; this stamp lands with the next
+ * batch, so it is read one batch late); and the host's submit -> done.
+ * Medians in microseconds. */
+static int ring_timeline(double seconds, struct mbuf *mb, uint32_t nmb, uint32_t maxk, const uint32_t *ref,
+                         const uint32_t *first)
+{
+    nc_gpuhash_ring_t *ring = nc_gpuhash_ring_create_ex(0, 1, maxk, MBUF_DATA, 1, 0);
+    if (!ring || nc_gpuhash_ring_debug_timeline(ring, 1, 0, NULL) != NC_OK) return 1;
+    uint32_t *outs = malloc(maxk * sizeof(uint32_t));
+    enum { NMAX = 200000, NV = 8 };
+    double *v[NV];
+    for (int i = 0; i < NV; i++) v[i] = malloc(NMAX * sizeof(double));
+    if (!outs) return 1;
+    uint64_t bad = 0, prev_stored = 0;
+    int n = 0;
+    const double tend = now_s() + seconds;
+    for (uint32_t i = 0; n < NMAX && now_s() < tend; i++) {
+        const uint32_t bi = i % nmb;
+        int tk;
+        const double a = now_s();
+        if (nc_gpuhash_ring_submit_spans(ring, NC_GPUHASH_FNV1A_64, mb[bi].spans, mb[bi].nkeys, outs, &tk) != NC_OK)
+            return 1;
+        const double b = now_s();
+        if (nc_gpuhash_ring_wait(ring, tk) != NC_OK) return 1;
+        const double c = now_s();
+        for (uint32_t k = 0; k < mb[bi].nkeys; k++) bad += outs[k] != ref[first[bi] + k];
+        uint64_t tl[8];
+        if (nc_gpuhash_ring_debug_timeline(ring, -1, 0, tl) != NC_OK) return 1;
+        const uint64_t stored = tl[3], released_prev = tl[4];
+        if (i >= nmb) { /* past the warm-up (the first launch) */
+            v[0][n] = (b - a) * 1e6;
+            v[1][n] = (c - a) * 1e6;
+            v[2][n] = (double)(tl[1] - tl[0]) * 0.01;
+            v[3][n] = (double)(tl[2] - tl[1]) * 0.01;
+            v[4][n] = (double)(tl[3] - tl[2]) * 0.01;
+            v[5][n] = (double)(tl[3] - tl[0]) * 0.01;
+            /* the previous batch's release, which landed with this one */
+            v[6][n] = released_prev > prev_stored && prev_stored ? (double)(released_prev - prev_stored) * 0.01 : 0.0;
+            v[7][n] = v[1][n] - v[0][n] - v[5][n] - v[6][n];
+            n++;
+        }
+        prev_stored = stored;
+    }
+    double med[NV];
+    for (int i = 0; i < NV; i++) {
+        qsort(v[i], (size_t)n, sizeof(double), cmp_d);
+        med[i] = n ? v[i][n / 2] : 0.0;
+    }
+    printf("{\"point\": \"ring_timeline\", \"depth\": 1, \"threads\": %d, \"batches\": %d, \"median_us\": "
+           "{\"host_submit_call\": %.2f, \"submit_to_done\": %.2f, \"dev_fetch\": %.2f, \"dev_hash\": %.2f, "
+           "\"dev_store_ack\": %.2f, \"dev_found_to_stored\": %.2f, \"dev_release\": %.2f, "
+           "\"rest_detect_done_reap\": %.2f}, \"mismatches\": %" PRIu64 "}\n",
+           NC_GPUHASH_RING_DEFAULT_THREADS, n, med[0], med[1], med[2], med[3], med[4], med[5], med[6], med[7], bad);
+    nc_gpuhash_ring_destroy(ring);
+    return bad ? 2 : 0;
+}
 
 int main(int argc, char **argv)
 {
@@ -117,6 +195,8 @@ int main(int argc, char **argv)
            "\"mbuf_fill_bytes\": %.1f, \"us_per_mbuf\": %.3f, \"mkeys_s\": %.2f, \"threads\": 1}\n",
            nmb, n, (double)n / nmb, (double)sum_len / nmb, host_s / nmb * 1e6, (double)n / host_s / 1e6);
     fflush(stdout);
+
+    if (argc > 2 && strcmp(argv[2], "timeline") == 0) return ring_timeline(seconds, mb, nmb, maxk, ref, first_of(mb, nmb));
 
     static const int depths[] = {1, 2, 4};
     int rc = 0;
@@ -189,21 +269,24 @@ int main(int argc, char **argv)
             free(outs);
         }
     }
-    /* the batch ring: the same loop over nc_gpuhash_ring_* */
-    static const int rdepths[] = {1, 2, 4, 8};
+    /* the batch ring: the same loop over nc_gpuhash_ring_*, one lane per
+     * batch in flight (up to 8), lane workgroups of 256 and 1024 threads */
+    static const int rdepths[] = {1, 2, 4, 8, 16};
+    static const uint32_t rthreads[] = {256, 1024};
+    for (size_t ti = 0; ti < sizeof(rthreads) / sizeof(rthreads[0]); ti++) {
     for (size_t di = 0; di < sizeof(rdepths) / sizeof(rdepths[0]); di++) {
         const int nslots = rdepths[di];
-        nc_gpuhash_ring_t *ring = nc_gpuhash_ring_create(0, (uint32_t)nslots, maxk, MBUF_DATA);
+        nc_gpuhash_ring_t *ring = nc_gpuhash_ring_create_ex(0, (uint32_t)nslots, maxk, MBUF_DATA, 0, rthreads[ti]);
         if (!ring) {
             fprintf(stderr, "ring_create failed\n");
             return 1;
         }
         uint32_t *outs = malloc((size_t)nslots * maxk * sizeof(uint32_t));
-        int tick[8];
-        uint32_t which[8];
-        double t_sub[8];
+        int tick[16];
+        uint32_t which[16];
+        double t_sub[16];
         if (!outs) return 1;
-        for (uint32_t i = 0; i < nmb; i++) { /* warm-up (the first submit launches the worker) */
+        for (uint32_t i = 0; i < nmb; i++) { /* warm-up (the first submit launches the workers) */
             int tk;
             if (nc_gpuhash_ring_submit_spans(ring, NC_GPUHASH_FNV1A_64, mb[i].spans, mb[i].nkeys, outs, &tk) != NC_OK ||
                 nc_gpuhash_ring_wait(ring, tk) != NC_OK)
@@ -243,14 +326,16 @@ int main(int argc, char **argv)
         }
         const double el = now_s() - t0;
         printf("{\"point\": \"gpu\", \"path\": \"ring (resident worker, mapped host memory)\", \"depth\": %d, "
+               "\"lanes\": %u, \"threads\": %u, "
                "\"batches\": %" PRIu64 ", \"keys_per_batch\": %.1f, \"submit_to_done_us\": %.2f, \"mkeys_s\": %.2f, "
                "\"mismatches\": %" PRIu64 ", \"worker_launches\": %" PRIu64 "}\n",
-               nslots, batches, (double)done_keys / (double)batches, lat_sum / (double)batches * 1e6,
-               (double)done_keys / el / 1e6, bad, nc_gpuhash_ring_launches(ring));
+               nslots, nc_gpuhash_ring_lanes(ring), rthreads[ti], batches, (double)done_keys / (double)batches,
+               lat_sum / (double)batches * 1e6, (double)done_keys / el / 1e6, bad, nc_gpuhash_ring_launches(ring));
         fflush(stdout);
         if (bad) rc = 2;
         nc_gpuhash_ring_destroy(ring);
         free(outs);
+    }
     }
     free(first);
     free(ref);

@@ -139,6 +139,15 @@ SIGNATURES = {
     "nc_gpuhash_ring_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "nc_gpuhash_ring_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "nc_gpuhash_ring_launches": (ctypes.c_uint64, [ctypes.c_void_p]),
+    "nc_gpuhash_ring_create_ex": (
+        ctypes.c_void_p,
+        [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32],
+    ),
+    "nc_gpuhash_ring_lanes": (ctypes.c_uint32, [ctypes.c_void_p]),
+    "nc_gpuhash_ring_debug_start_seq": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "nc_gpuhash_ring_debug_hold": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "nc_gpuhash_ring_debug_timeline": (
+        ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
     "nc_gpuhash_frag_plan": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],

@@ -30,10 +30,11 @@ constexpr bool is_crc()
     return MODE == NC_GPUHASH_CRC16 || MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A;
 }
 
-template <uint32_t R>
+/* NT tables (4: slicing-by-4; 8: slicing-by-8) of 256 entries, R copies */
+template <uint32_t R, uint32_t NT = 4>
 constexpr uint32_t table_words()
 {
-    return 4u * 256u * R;
+    return NT * 256u * R;
 }
 
 /* entry e of table k */
@@ -52,10 +53,10 @@ __device__ __forceinline__ uint32_t entry(uint32_t k, uint32_t e)
 }
 
 /* fill the R-copy tables at tab, threads t = first, first + step, ... */
-template <int MODE, uint32_t R>
+template <int MODE, uint32_t R, uint32_t NT = 4>
 __device__ __forceinline__ void fill(uint32_t *tab, uint32_t first, uint32_t step)
 {
-    for (uint32_t i = first; i < 4u * 256u; i += step) {
+    for (uint32_t i = first; i < NT * 256u; i += step) {
         const uint32_t v = entry<MODE>(i >> 8, i & 255u);
 #pragma unroll
         for (uint32_t c = 0; c < R; c++) tab[i * R + c] = v;
@@ -104,6 +105,30 @@ __device__ __forceinline__ uint32_t word(uint32_t h, uint32_t w, const uint32_t 
         const uint32_t x = h ^ w;
         return look<R>(tab, x >> 24, cb, 0) ^ look<R>(tab, (x >> 16) & 0xffu, cb, 1) ^
                look<R>(tab, (x >> 8) & 0xffu, cb, 2) ^ look<R>(tab, x & 0xffu, cb, 3);
+    }
+}
+
+/* the 8 bytes of words w0, w1 (slicing-by-8: eight independent lookups, half
+ * the dependent steps of slicing-by-4); tables 0..7 */
+template <int MODE, uint32_t R>
+__device__ __forceinline__ uint32_t word2(uint32_t h, uint32_t w0, uint32_t w1, const uint32_t *tab, uint32_t cb)
+{
+    if constexpr (MODE == NC_GPUHASH_CRC16) {
+        /* MSB first: the state meets the first two bytes; byte i of the 8
+         * goes through table 7 - i (the history bits: as in word()) */
+        const uint32_t v = ((h & 0xffffu) << 16) ^ __builtin_bswap32(w0);
+        const uint32_t u = __builtin_bswap32(w1);
+        return (look<R>(tab, v >> 24, cb, 7) ^ look<R>(tab, (v >> 16) & 0xffu, cb, 6)) ^
+               (look<R>(tab, (v >> 8) & 0xffu, cb, 5) ^ look<R>(tab, v & 0xffu, cb, 4)) ^
+               (look<R>(tab, u >> 24, cb, 3) ^ look<R>(tab, (u >> 16) & 0xffu, cb, 2)) ^
+               (look<R>(tab, (u >> 8) & 0xffu, cb, 1) ^ look<R>(tab, u & 0xffu, cb, 0));
+    } else {
+        /* reflected: byte i of the 8 (LSB of w0 first) through table 7 - i */
+        const uint32_t x = h ^ w0;
+        return (look<R>(tab, x & 0xffu, cb, 7) ^ look<R>(tab, (x >> 8) & 0xffu, cb, 6)) ^
+               (look<R>(tab, (x >> 16) & 0xffu, cb, 5) ^ look<R>(tab, x >> 24, cb, 4)) ^
+               (look<R>(tab, w1 & 0xffu, cb, 3) ^ look<R>(tab, (w1 >> 8) & 0xffu, cb, 2)) ^
+               (look<R>(tab, (w1 >> 16) & 0xffu, cb, 1) ^ look<R>(tab, w1 >> 24, cb, 0));
     }
 }
 

@@ -35,6 +35,7 @@
 #include "nc_gpuhash_probe.h"
 #include "nc_hash_algo.h"
 #include "nc_md5_steps.h"
+#include "nc_lds_hash.h"
 
 namespace {
 
@@ -64,450 +65,6 @@ static_assert(kSmemBytes <= kLdsBudget, "LDS budget");
 static_assert(kSlabCap >= 8192 + 48, "a 256 x 32 B tile must fit one slab buffer");
 static_assert(kSlabCap < 65536, "sorted key positions are packed in 16 bits");
 static_assert(kOffTab % 16 == 0, "LDS carve must stay 16-byte aligned");
-
-/* ---------------- realigning readers ---------------- */
-
-struct LdsSrc {
-    typedef uint32_t pos_t;
-    static constexpr bool kOverread = true; /* reads past a key stay inside LDS */
-    const uint32_t *base; /* 16-byte aligned LDS slab, read as dwords */
-    /* dwords i, i+1 (4-byte aligned): one ds_read2_b32 */
-    __device__ __forceinline__ uint2 d2(uint32_t i) const { return make_uint2(base[i], base[i + 1]); }
-    __device__ __forceinline__ uint32_t d1(uint32_t i) const { return base[i]; }
-};
-
-struct GlobalSrc {
-    typedef uint64_t pos_t;
-    static constexpr bool kOverread = false; /* at most NC_GPUHASH_PAD past the last key */
-    const uint32_t *base; /* 16-byte aligned key buffer */
-    __device__ __forceinline__ uint2 d2(uint64_t i) const { return make_uint2(base[i], base[i + 1]); }
-    __device__ __forceinline__ uint32_t d1(uint64_t i) const { return base[i]; }
-};
-
-/* Sequential little-endian words of a byte string starting at any byte
- * position p: aligned dwords funnel-shifted by (p & 3) bytes with
- * v_alignbyte_b32; one ds_read2_b32 per 8 bytes, no selects. Reads at most
- * 14 bytes past the end of the string (covered by the staged look-ahead
- * piece / NC_GPUHASH_PAD). */
-template <class Src, bool kDeep = false>
-struct QStream {
-    /* kDeep (LDS only): reads run two steps ahead, so a step never waits for
-     * the read the previous step issued */
-    static constexpr bool D2 = kDeep && Src::kOverread;
-    Src src;
-    typename Src::pos_t di;
-    uint32_t sh;
-    uint32_t prev;
-    uint2 ahead;  /* dwords di+1, di+2, read one step early */
-    uint2 ahead2; /* dwords di+3, di+4 (D2 only) */
-
-    __device__ __forceinline__ void init(const Src &s, typename Src::pos_t p)
-    {
-        src = s;
-        di = p >> 2;
-        sh = (uint32_t)p & 3u;
-        prev = src.d1(di);
-        ahead = src.d2(di + 1);
-        if constexpr (D2) ahead2 = src.d2(di + 3);
-    }
-    /* next 8 bytes as two words; the read for the following 8 is issued now
-     * (it may touch up to 22 bytes past the string: inside the staged
-     * look-ahead piece / NC_GPUHASH_PAD) */
-    __device__ __forceinline__ uint2 next8()
-    {
-        const uint2 d = ahead;
-        di += 2;
-        if constexpr (D2) {
-            ahead = ahead2;
-            ahead2 = src.d2(di + 3);
-            asm volatile("" ::: "memory"); /* keep the read here, not at its use */
-        } else {
-            ahead = src.d2(di + 1);
-        }
-        uint2 r;
-        r.x = __builtin_amdgcn_alignbyte(d.x, prev, sh);
-        r.y = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
-        prev = d.y;
-        return r;
-    }
-};
-
-/* One word at a time on top of QStream (word-granular modes). */
-template <class Src>
-struct WStream {
-    QStream<Src> q;
-    uint32_t pend;
-    bool has;
-    __device__ __forceinline__ void init(const Src &s, typename Src::pos_t p)
-    {
-        q.init(s, p);
-        has = false;
-        pend = 0;
-    }
-    __device__ __forceinline__ uint32_t next()
-    {
-        if (has) {
-            has = false;
-            return pend;
-        }
-        uint2 r = q.next8();
-        pend = r.y;
-        has = true;
-        return r.x;
-    }
-};
-
-__device__ __forceinline__ uint32_t keep_bytes(uint32_t w, uint32_t nb)
-{
-    return nb >= 4u ? w : (nb == 0u ? 0u : (w & (0xffffffffu >> (32u - 8u * nb))));
-}
-
-/* ---------------- byte-serial modes ---------------- */
-
-template <int MODE>
-__device__ __forceinline__ uint32_t byte_init()
-{
-    if constexpr (MODE == NC_GPUHASH_FNV1_64 || MODE == NC_GPUHASH_FNV1A_64) return NC_FNV64_INIT32;
-    if constexpr (MODE == NC_GPUHASH_FNV1_32 || MODE == NC_GPUHASH_FNV1A_32) return NC_FNV32_INIT;
-    if constexpr (MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A) return 0xffffffffu;
-    return 0u; /* one_at_a_time, crc16 */
-}
-
-/* Shift counts the compiler cannot see through: with them, (h << s1) + h
- * stays three full-rate v_lshl_add_u32 (3h, 27h, 435h = h * 0x1b3) instead of
- * being folded back into the multi-pass v_mul_lo_u32, and — unlike inline asm
- * — the instructions stay visible to the scheduler and hazard recognizer. */
-struct ShiftK {
-    uint32_t s1, s3, s4;
-};
-__device__ __forceinline__ ShiftK opaque_shifts()
-{
-    ShiftK k;
-    asm volatile("s_mov_b32 %0, 1" : "=s"(k.s1));
-    asm volatile("s_mov_b32 %0, 3" : "=s"(k.s3));
-    asm volatile("s_mov_b32 %0, 4" : "=s"(k.s4));
-    return k;
-}
-__device__ __forceinline__ uint32_t mul_0x1b3(uint32_t h, const ShiftK &k)
-{
-    const uint32_t t3 = (h << k.s1) + h;
-    const uint32_t t27 = (t3 << k.s3) + t3;
-    return (t27 << k.s4) + t3;
-}
-
-/* VAR bit 0: FNV-64-truncated multiply by shift-adds. */
-template <int MODE, int VAR = 0>
-__device__ __forceinline__ uint32_t byte_step(uint32_t h, uint32_t b, const uint32_t *tab, const ShiftK &k)
-{
-    if constexpr (MODE == NC_GPUHASH_FNV1A_64 && (VAR & 1)) return mul_0x1b3(h ^ nc_sx8(b), k);
-    if constexpr (MODE == NC_GPUHASH_FNV1_64 && (VAR & 1)) return mul_0x1b3(h, k) ^ nc_sx8(b);
-    if constexpr (MODE == NC_GPUHASH_FNV1A_64) return nc_fnv1a_64_step(h, b);
-    if constexpr (MODE == NC_GPUHASH_FNV1_64) return nc_fnv1_64_step(h, b);
-    if constexpr (MODE == NC_GPUHASH_FNV1_32) return nc_fnv1_32_step(h, b);
-    if constexpr (MODE == NC_GPUHASH_FNV1A_32) return nc_fnv1a_32_step(h, b);
-    if constexpr (MODE == NC_GPUHASH_ONE_AT_A_TIME) return nc_oaat_step(h, b);
-    if constexpr (MODE == NC_GPUHASH_CRC16) return NC_CRC16_NEXT(h, tab[NC_CRC16_IDX(h, b)]);
-    if constexpr (MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A) return NC_CRC32_NEXT(h, tab[NC_CRC32_IDX(h, b)]);
-    return h;
-}
-
-template <int MODE>
-__device__ __forceinline__ uint32_t byte_final(uint32_t h)
-{
-    if constexpr (MODE == NC_GPUHASH_ONE_AT_A_TIME) return nc_oaat_final(h);
-    if constexpr (MODE == NC_GPUHASH_CRC32) return nc_crc32_final(h);
-    if constexpr (MODE == NC_GPUHASH_CRC32A) return nc_crc32a_final(h);
-    return h;
-}
-
-template <int MODE, int VAR>
-__device__ __forceinline__ uint32_t word_bytes(uint32_t h, uint32_t w, const uint32_t *tab, const ShiftK &k)
-{
-    h = byte_step<MODE, VAR>(h, w & 0xffu, tab, k);
-    h = byte_step<MODE, VAR>(h, (w >> 8) & 0xffu, tab, k);
-    h = byte_step<MODE, VAR>(h, (w >> 16) & 0xffu, tab, k);
-    h = byte_step<MODE, VAR>(h, w >> 24, tab, k);
-    return h;
-}
-
-template <int MODE, int VAR, class Src>
-__device__ __forceinline__ uint32_t hash_bytes(const Src &src, typename Src::pos_t p, uint32_t len,
-                                               const uint32_t *tab)
-{
-    ShiftK k{0u, 0u, 0u};
-    if constexpr ((VAR & 1) != 0) k = opaque_shifts();
-    QStream<Src, (VAR & 1024) != 0> st;
-    st.init(src, p);
-    uint32_t h = byte_init<MODE>();
-    const uint32_t n8 = len >> 3;
-#pragma unroll 2
-    for (uint32_t i = 0; i < n8; i++) {
-        uint2 w = st.next8();
-        h = word_bytes<MODE, VAR>(h, w.x, tab, k);
-        h = word_bytes<MODE, VAR>(h, w.y, tab, k);
-    }
-    const uint32_t rem = len & 7u;
-    if (rem) {
-        uint2 w = st.next8();
-        if (rem >= 4) {
-            h = word_bytes<MODE, VAR>(h, w.x, tab, k);
-            w.x = w.y;
-        }
-        for (uint32_t j = 0; j < (rem & 3u); j++) {
-            h = byte_step<MODE, VAR>(h, (w.x >> (8u * j)) & 0xffu, tab, k);
-        }
-    }
-    return byte_final<MODE>(h);
-}
-
-/* Two keys of one lane hashed in one loop, so the two dependent chains
- * interleave (ILP for the latency-bound byte recurrences). LDS only: the
- * shorter key's stream reads on past its end (garbage bytes, never used). */
-template <int MODE, int VAR>
-__device__ __forceinline__ void hash_bytes_pair(const LdsSrc &src, uint32_t pa, uint32_t la, uint32_t pb,
-                                                uint32_t lb, const uint32_t *tab, uint32_t &ra, uint32_t &rb)
-{
-    ShiftK k{0u, 0u, 0u};
-    if constexpr ((VAR & 1) != 0) k = opaque_shifts();
-    QStream<LdsSrc, (VAR & 1024) != 0> sa, sb;
-    sa.init(src, pa);
-    sb.init(src, pb);
-    uint32_t ha = byte_init<MODE>(), hb = ha;
-    const uint32_t na = la >> 3, nb = lb >> 3;
-    const uint32_t nmax = na > nb ? na : nb;
-    for (uint32_t i = 0; i < nmax; i++) {
-        const uint2 wa = sa.next8(), wb = sb.next8();
-        uint32_t xa = ha, xb = hb;
-        /* byte-granular alternation: in-order issue overlaps the two chains
-         * only if their steps alternate in the instruction stream */
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-            const uint32_t va = ((b < 4 ? wa.x : wa.y) >> (8 * (b & 3))) & 0xffu;
-            const uint32_t vb = ((b < 4 ? wb.x : wb.y) >> (8 * (b & 3))) & 0xffu;
-            xa = byte_step<MODE, VAR>(xa, va, tab, k);
-            xb = byte_step<MODE, VAR>(xb, vb, tab, k);
-        }
-        if (i < na) ha = xa;
-        if (i < nb) hb = xb;
-    }
-    /* tails: each key's stream is re-anchored on its tail */
-    auto tail = [&](uint32_t h, uint32_t p, uint32_t len) __attribute__((always_inline)) {
-        const uint32_t rem = len & 7u;
-        if (rem) {
-            QStream<LdsSrc> st;
-            st.init(src, p + (len & ~7u));
-            uint2 w = st.next8();
-            if (rem >= 4) {
-                h = word_bytes<MODE, VAR>(h, w.x, tab, k);
-                w.x = w.y;
-            }
-            for (uint32_t j = 0; j < (rem & 3u); j++) h = byte_step<MODE, VAR>(h, (w.x >> (8u * j)) & 0xffu, tab, k);
-        }
-        return byte_final<MODE>(h);
-    };
-    ra = tail(ha, pa, la);
-    rb = tail(hb, pb, lb);
-}
-
-/* ---------------- word-granular modes ---------------- */
-
-template <class Src>
-__device__ __forceinline__ uint32_t hash_hsieh_dev(const Src &src, typename Src::pos_t p, uint32_t len)
-{
-    if (len == 0) return 0; /* nc_hsieh.c:44 */
-    QStream<Src> st;
-    st.init(src, p);
-    uint32_t h = 0;
-    const uint32_t nw = len >> 2;
-    for (uint32_t i = 0; i < (nw >> 1); i++) {
-        uint2 w = st.next8();
-        h = nc_hsieh_word(h, w.x);
-        h = nc_hsieh_word(h, w.y);
-    }
-    const uint32_t rem = len & 3u;
-    if ((nw & 1u) || rem) {
-        uint2 w = st.next8();
-        uint32_t tail = w.x;
-        if (nw & 1u) {
-            h = nc_hsieh_word(h, w.x);
-            tail = w.y;
-        }
-        h = nc_hsieh_tail(h, tail, rem);
-    }
-    return nc_hsieh_final(h);
-}
-
-template <class Src>
-__device__ __forceinline__ uint32_t hash_murmur_dev(const Src &src, typename Src::pos_t p, uint32_t len)
-{
-    QStream<Src> st;
-    st.init(src, p);
-    uint32_t h = nc_murmur_init(len);
-    const uint32_t nw = len >> 2;
-    for (uint32_t i = 0; i < (nw >> 1); i++) {
-        uint2 w = st.next8();
-        h = nc_murmur_word(h, w.x);
-        h = nc_murmur_word(h, w.y);
-    }
-    const uint32_t rem = len & 3u;
-    if ((nw & 1u) || rem) {
-        uint2 w = st.next8();
-        uint32_t tail = w.x;
-        if (nw & 1u) {
-            h = nc_murmur_word(h, w.x);
-            tail = w.y;
-        }
-        h = nc_murmur_tail(h, tail, rem);
-    }
-    return nc_murmur_final(h);
-}
-
-template <class Src>
-__device__ __forceinline__ uint32_t hash_jenkins_dev(const Src &src, typename Src::pos_t p, uint32_t len)
-{
-    uint32_t a, b, c;
-    a = b = c = nc_jenkins_init(len);
-    if (len == 0) return c; /* nc_jenkins.c:121 */
-    WStream<Src> ws;
-    ws.init(src, p);
-    uint32_t n = len;
-    while (n > 12) {
-        a += ws.next();
-        b += ws.next();
-        c += ws.next();
-        NC_JENKINS_MIX(a, b, c);
-        n -= 12;
-    }
-    /* last 1..12 bytes, zero-extended */
-    a += keep_bytes(ws.next(), n);
-    if (n > 4) b += keep_bytes(ws.next(), n - 4);
-    if (n > 8) c += keep_bytes(ws.next(), n - 8);
-    NC_JENKINS_FINAL(a, b, c);
-    return c;
-}
-
-template <class Src>
-__device__ __forceinline__ uint32_t hash_md5_dev(const Src &src, typename Src::pos_t p, uint32_t len)
-{
-    QStream<Src> st;
-    st.init(src, p);
-    uint32_t s[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
-    uint32_t w[16];
-    const uint32_t nfull = len >> 6;
-    for (uint32_t blk = 0; blk < nfull; blk++) {
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            uint2 r = st.next8();
-            w[2 * t] = r.x;
-            w[2 * t + 1] = r.y;
-        }
-        nc_md5_block(s, w);
-    }
-    /* final block(s): remaining rem bytes, 0x80, zeros, 64-bit bit length.
-     * Word t is raw for t < q, the partial word | 0x80 pad for t == q, and 0
-     * after it (q = rem / 4). From LDS all 8 reads are unconditional (no
-     * per-lane branches; over-read bytes are masked off here). */
-    const uint32_t rem = len & 63u;
-    const uint32_t q = rem >> 2;
-    const uint32_t sh = (rem & 3u) << 3;
-    const uint32_t keep = (1u << sh) - 1u; /* low rem%4 bytes of the partial word */
-    const uint32_t pad = 0x80u << sh;
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        uint2 r = make_uint2(0u, 0u);
-        if constexpr (Src::kOverread) r = st.next8();
-        else if (8u * t < rem) r = st.next8();
-        const uint32_t t0 = 2u * t, t1 = 2u * t + 1u;
-        w[t0] = t0 < q ? r.x : (t0 == q ? ((r.x & keep) | pad) : 0u);
-        w[t1] = t1 < q ? r.y : (t1 == q ? ((r.y & keep) | pad) : 0u);
-    }
-    const uint64_t bits = (uint64_t)len << 3;
-    if (rem >= 56) {
-        nc_md5_block(s, w);
-#pragma unroll
-        for (int t = 0; t < 16; t++) w[t] = 0;
-    }
-    w[14] = (uint32_t)bits;
-    w[15] = (uint32_t)(bits >> 32);
-    nc_md5_block(s, w);
-    return s[0]; /* digest bytes 0..3 little-endian (nc_md5.c:317-320) */
-}
-
-/* Message words of block `blk` of a key of `len` bytes read from `st`: the
- * key's bytes, then 0x80, zeros and, in its last block, the bit length
- * (src/hashkit/nc_md5.c:245-274). LDS only: the reads run past the key. */
-__device__ __forceinline__ void md5_words(QStream<LdsSrc> &st, uint32_t w[16], uint32_t len, uint32_t blk)
-{
-    const int32_t rem = (int32_t)len - 64 * (int32_t)blk; /* message bytes from the block start */
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const uint2 r = st.next8();
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint32_t v = h ? r.y : r.x;
-            const int32_t nb = rem - (8 * t + 4 * h); /* message bytes in this word */
-            const uint32_t part = nb <= 0 ? 0u : (v & (0xffffffffu >> (32u - 8u * (uint32_t)nb)));
-            const uint32_t pad = (nb >= 0 && nb < 4) ? (0x80u << (8u * (uint32_t)nb)) : 0u;
-            w[2 * t + h] = nb >= 4 ? v : (part | pad);
-        }
-    }
-    if (blk == (len + 8u) / 64u) { /* the last block */
-        w[14] = len << 3;
-        w[15] = len >> 29;
-    }
-}
-
-/* md5 of a lane's two keys with their blocks interleaved step by step
- * (nc_md5_block2): two independent chains per lane instead of one. */
-__device__ __forceinline__ void hash_md5_pair(const LdsSrc &src, uint32_t pa, uint32_t la, uint32_t pb,
-                                              uint32_t lb, uint32_t &ra, uint32_t &rb)
-{
-    QStream<LdsSrc> sa, sb;
-    sa.init(src, pa);
-    sb.init(src, pb);
-    uint32_t A[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
-    uint32_t B[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
-    const uint32_t na = (la + 8u) / 64u + 1u, nb = (lb + 8u) / 64u + 1u;
-    const uint32_t n = na > nb ? na : nb;
-    for (uint32_t blk = 0; blk < n; blk++) {
-        uint32_t wa[16], wb[16];
-        md5_words(sa, wa, la, blk);
-        md5_words(sb, wb, lb, blk);
-        uint32_t ta[4] = {A[0], A[1], A[2], A[3]}, tb[4] = {B[0], B[1], B[2], B[3]};
-        nc_md5_block2(ta, wa, tb, wb);
-        if (blk < na) {
-            A[0] = ta[0];
-            A[1] = ta[1];
-            A[2] = ta[2];
-            A[3] = ta[3];
-        }
-        if (blk < nb) {
-            B[0] = tb[0];
-            B[1] = tb[1];
-            B[2] = tb[2];
-            B[3] = tb[3];
-        }
-    }
-    ra = A[0]; /* digest bytes 0..3 little-endian (nc_md5.c:317-320) */
-    rb = B[0];
-}
-
-template <int MODE, int VAR, class Src>
-__device__ __forceinline__ uint32_t hash_key(const Src &src, typename Src::pos_t p, uint32_t len,
-                                             const uint32_t *tab)
-{
-    if constexpr (MODE == NC_GPUHASH_MD5) return hash_md5_dev(src, p, len);
-    else if constexpr (MODE == NC_GPUHASH_HSIEH) return hash_hsieh_dev(src, p, len);
-    else if constexpr (MODE == NC_GPUHASH_MURMUR) return hash_murmur_dev(src, p, len);
-    else if constexpr (MODE == NC_GPUHASH_JENKINS) return hash_jenkins_dev(src, p, len);
-    else return hash_bytes<MODE, VAR>(src, p, len, tab);
-}
-
-template <int MODE>
-constexpr bool uses_crc_table()
-{
-    return MODE == NC_GPUHASH_CRC16 || MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A;
-}
 
 /* Length class used to group keys of similar cost into one wave. */
 __device__ __forceinline__ uint32_t len_bucket(uint32_t len)
@@ -2014,7 +1571,8 @@ constexpr bool wr_sorted()
 template <int MODE, int DIST, int P, int DS, int DO, int WPW, int TK = kWrTile, int VAR = 0>
 constexpr uint32_t wr_lds_fixed()
 {
-    return (uint32_t)WPW * WrRing<P, DS, DO, TK, wr_sorted<VAR, TK>()>::kBytes + (uses_crc_table<MODE>() ? 1024u : 0u);
+    return (uint32_t)WPW * WrRing<P, DS, DO, TK, wr_sorted<VAR, TK>()>::kBytes +
+           (uses_crc_table<MODE>() ? ((VAR & kHkCrcSliced) != 0 ? 1024u * kSliceTables : 1024u) : 0u);
 }
 
 template <int MODE, int VAR, int P, int DS, int DO, int DIST, int WPW, int TK = kWrTile>
@@ -2040,7 +1598,9 @@ __global__ __launch_bounds__(64 * WPW) void nc_hash_kernel_wr(const uint8_t *__r
     uint32_t *cont = reinterpret_cast<uint32_t *>(wr_lds + kContOffs);
 
     /* shared set-up, before any DMA is in flight */
-    if constexpr (uses_crc_table<MODE>()) {
+    if constexpr (uses_crc_table<MODE>() && (VAR & kHkCrcSliced) != 0) {
+        for (uint32_t i = t; i < 256u * kSliceTables; i += 64u * WPW) tab[i] = nc_slice::entry<MODE>(i >> 8, i & 255u);
+    } else if constexpr (uses_crc_table<MODE>()) {
         for (uint32_t i = t; i < 256u; i += 64u * WPW)
             tab[i] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(i) : nc_crc32_entry(i);
     }
@@ -2372,7 +1932,14 @@ constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline sta
 constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 4 sentinels), beside four 512-key
                                             workgroups per CU */
 constexpr int kVarNoPacked = 1 << 27; /* server_idx A/B: the 5-byte LDS continuum even where the packed one fits */
-constexpr int kVarDirect8 = 1 << 27; /* direct byte kernels, line image: eight-wave workgroups, one per CU */
+/* direct byte kernels' options beyond bits 20-23, in bits only the ring
+ * pipeline reads otherwise (bit 19 selects the direct pipeline first) */
+constexpr int kVarDirect8 = 1 << 12;     /* line image: eight-wave workgroups, one per CU */
+constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
+constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
+static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash) &
+               (kVarMd5Direct | (15 << 20) | kVarNoFixedLen | kVarWsort | kVarGsort | kVarNoPacked | (3 << 29))) == 0,
+              "direct-pipeline options overlap the pipeline choice, its nibble or the server_idx bits");
 
 int load_i(const int *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 void store_i(int *p, int v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
@@ -2681,6 +2248,19 @@ hipError_t launch_wr_mode(const uint8_t *base, const uint64_t *off, uint64_t del
     if constexpr (has_mul_variant(MODE)) { /* shift-add multiply: default ring shape only */
         if (var & 1) return launch_wr_plain<MODE, 1, 4, 2, 3>(base, off, delta, nkeys, out, stream);
     }
+    if constexpr (uses_crc_table<MODE>()) {
+        /* bit 11: slicing-by-16 tables (16 KiB) shared by the workgroup's
+         * waves; bits 12-13 the ring: P5 x 7 waves, P5 x 6, P5 x 4, P4 x 8 */
+        if (var & 2048) {
+            constexpr int V = kHkCrcSliced;
+            switch ((var >> 12) & 3) {
+            case 0: return launch_wr_plain<MODE, V, 5, 2, 3, 7>(base, off, delta, nkeys, out, stream);
+            case 1: return launch_wr_plain<MODE, V, 5, 2, 3, 6>(base, off, delta, nkeys, out, stream);
+            case 2: return launch_wr_plain<MODE, V, 5, 2, 3, 4>(base, off, delta, nkeys, out, stream);
+            default: return launch_wr_plain<MODE, V, 4, 2, 3, 8>(base, off, delta, nkeys, out, stream);
+            }
+        }
+    }
     return launch_wr_hash<MODE, 0>(base, off, delta, nkeys, out, stream, var);
 }
 
@@ -2914,7 +2494,8 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
         }
         if (nc_bytes::supports(mode))
             return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream,
-                                    ((var >> 20) & 15) | ((var & kVarDirect8) != 0 ? 16 : 0));
+                                    ((var >> 20) & 15) | ((var & kVarDirect8) != 0 ? 16 : 0) |
+                                        ((var & kVarDirectS8) != 0 ? 32 : 0) | ((var & kVarDirectNoHash) != 0 ? 64 : 0));
     }
     if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))
         return nc_wsort::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);

@@ -5,38 +5,53 @@
  * The context path (nc_gpuhash_submit_spans) spends ~5 µs of host time per
  * batch in hipLaunchKernel and hipEventRecord, and the device idles between
  * batches. Here the batch ring lives in mapped, coherent
- * host memory and resident worker workgroups serve it:
+ * host memory and ONE resident launch serves it, one workgroup per lane:
  *
- *   lanes: batch `seq` belongs to lane seq % kLanes, and each lane has its
- *     own worker, so one lane's PCIe round trips (fetch the batch, store the
- *     hashes) overlap the other's; every lane walks the same slots.
+ *   lanes: batch `seq` belongs to lane seq % nlanes (up to kMaxLanes), and
+ *     each lane's workgroup takes its batches in order, so the lanes' PCIe
+ *     round trips (find the batch, fetch it, store the hashes) overlap; every
+ *     lane walks the same slots. One launch on one stream (not a stream per
+ *     lane): streams share the process's few hardware queues, and a resident
+ *     kernel blocks whatever queues behind it.
  *   host submit: copy the bytes under the spans into the slot's staging —
  *     the mbuf region they cover in ONE memcpy when it fits (the keys of a
  *     read are contiguous in their mbuf, src/nc_mbuf.h:25-40), else key by
  *     key — with one u32 per key (its start and end in the staged image, 16
  *     bits each), then publish the slot with ONE 64-bit store of its
- *     descriptor: sequence number + 1 in the high word, mode / key count /
- *     key bytes packed in the low word (release). No HIP call while the
- *     worker runs.
- *   worker: thread 0 polls the next slot's descriptor (one system-scope
- *     acquire load across PCIe per poll, s_sleep between polls): the load
+ *     descriptor: the batch's tag in the high word, mode / key count / key
+ *     bytes packed in the low word. No HIP call while the workers run.
+ *   tags: tag(seq) = 2^31 | (seq mod 2^31), never 0 (a slot never used), and
+ *     two batches of one slot within 2^31 of each other never share one. The
+ *     host numbers batches with a 64-bit seq; a worker carries its next
+ *     slot and tag forward by nlanes (no 32-bit product that could wrap), and
+ *     its 64-bit `processed` count places a relaunch.
+ *   worker: thread 0 polls its next slot's descriptor together with `stop`
+ *     and the launch's `closing` word (relaxed loads, one round trip per
+ *     poll; the acquire fence only once the descriptor matches); the load
  *     that finds the slot published also carries the batch's shape. The
- *     workgroup stages the slot's offsets and key bytes into LDS with
- *     coalesced 16-byte reads across PCIe, all of them in flight at once,
- *     every thread hashes
- *     keys from LDS with the per-key functions (nc_hash_key.h: all 12
- *     modes), writes the hashes to the slot's mapped output, fences at system
- *     scope, and thread 0 stores the slot's completion word (release).
+ *     workgroup stages the slot's spans and key bytes into LDS with
+ *     coalesced 16-byte reads across PCIe, all in flight at once, every
+ *     thread hashes keys from LDS with the batch kernels' realigning word
+ *     readers (nc_lds_hash.h: aligned dwords + v_alignbyte, reads a step
+ *     ahead, all 12 modes; byte-at-a-time LDS reads would put one LDS
+ *     latency on every key byte), writes the hashes to the slot's mapped
+ *     output, and
+ *     thread 0 issues one system-scope release and the slot's done word.
  *   host poll: one load of that word; the hashes are copied to the caller.
  *
- * The worker always ends: it returns when `stop` is set, after kIdleTicks of
- * an empty ring, and after kLifeTicks in any case (s_memrealtime, 100 MHz).
- * Leaving is race-free: the worker publishes `exiting`, fences, then looks at
- * the next slot's descriptor once more; the host publishes the descriptor,
- * fences, then looks at `exiting`. At least one of them sees the other, so a batch is either taken
- * by the leaving worker or the host knows to relaunch one (only once the
- * previous launch has completed: never two workers on one lane). A relaunch
- * starts at `processed`, the lane's count of finished batches.
+ * The launch always ends: on `stop`; and once any lane finds the whole ring
+ * idle for kIdleTicks, or the launch older than kLifeTicks (checked before
+ * every batch, under load too), it sets the launch's `closing` word and
+ * every lane leaves. Leaving is race-free per lane: the worker publishes its
+ * lane's `exiting`, fences, then looks at its next slot's descriptor again
+ * (and serves it if published); the host publishes a descriptor, fences,
+ * then looks at that lane's `exiting`. At least one of them sees the other,
+ * so a batch is either served by the leaving worker or the host knows to
+ * relaunch — only once the previous launch has completed (its event), never
+ * two workers on one lane. A relaunch starts each lane at its `processed`.
+ * A batch published while its lane is leaving is therefore served on the
+ * next submit or poll that finds the launch finished: poll (or wait) every
+ * ticket.
  */
 #include <hip/hip_runtime.h>
 
@@ -49,41 +64,59 @@
 #include <time.h>
 
 #include "nc_gpuhash.h"
-#include "nc_hash_key.h"
+#include "nc_gpuhash_probe.h"
+#include "nc_hash_algo.h"
+#include "nc_lds_hash.h"
 
 namespace {
 
-constexpr uint32_t kThreads = 1024;          /* the worker: one workgroup of 16 waves */
-constexpr uint64_t kIdleTicks = 1000000ull;  /* 10 ms without a batch: the worker leaves */
-constexpr uint64_t kLifeTicks = 200000000ull; /* 2 s: no worker outlives this (relaunched on demand) */
-constexpr uint32_t kMaxKeys = 4095;          /* per batch: offsets in LDS */
-constexpr uint64_t kMaxKeyBytes = 32768;     /* per batch: key bytes in LDS */
-constexpr uint32_t kLanes = 2;               /* workers per ring (a power of two) */
+constexpr uint64_t kIdleTicks = 1000000ull;   /* 10 ms without a batch on any lane: the launch ends */
+constexpr uint64_t kLifeTicks = 200000000ull; /* 2 s: no launch outlives this (relaunched on demand) */
+constexpr uint32_t kMaxKeys = 4095;           /* per batch: offsets in LDS */
+constexpr uint64_t kMaxKeyBytes = 32768;      /* per batch: key bytes in LDS */
+constexpr uint32_t kMaxLanes = 8;             /* workgroups per launch */
+constexpr uint32_t kTagBit = 0x80000000u, kTagMask = 0x7fffffffu;
+static_assert(kMaxLanes == NC_GPUHASH_RING_MAX_LANES, "header limit");
 
-/* the control block, host-written and device-written words on their own
- * 128-byte lines */
+/* a lane's control block in mapped host memory: host-written and
+ * device-written words on their own 128-byte lines */
 struct RingCtl {
-    uint32_t head; /* host: the lane's batches submitted (for the host's own checks) */
     uint32_t stop; /* host: 1 = the worker returns at its next poll */
-    uint32_t pad0[30];
-    uint32_t exiting;   /* device: 1 from the moment a worker decides to leave */
-    uint32_t processed; /* device: batches finished, in order */
-    uint32_t pad1[30];
+    uint32_t pad0[31];
+    uint32_t exiting;   /* device: 1 from the moment the lane's worker decides to leave */
+    uint32_t pad1;
+    uint64_t processed; /* device: the lane's batches finished, in order (a 64-bit lane-local count) */
+    uint32_t pad2[28];
+};
+static_assert(sizeof(RingCtl) == 256, "two lines per lane");
+
+/* the launch's shared state, in device memory (workgroups of one launch) */
+struct RingDev {
+    uint64_t last; /* s_memrealtime of the latest finished batch on any lane */
+    uint32_t closing; /* = the launch's epoch once the launch is ending */
+    uint32_t pad;
 };
 
-/* a slot's descriptor, written by the host in ONE 64-bit store: batch
- * sequence number + 1 (0 = never used) over mode (4 bits), keys (12 bits) and
- * key bytes (16 bits: up to kMaxKeyBytes) */
-__host__ __device__ inline uint64_t desc_pack(uint32_t seq, uint32_t mode, uint32_t nkeys, uint32_t nbytes)
+__host__ __device__ inline uint32_t ring_tag(uint64_t seq) { return kTagBit | (uint32_t)(seq & kTagMask); }
+
+/* a slot's descriptor, written by the host in ONE 64-bit store: the batch's
+ * tag over mode (4 bits), keys (12 bits) and key bytes (16 bits: up to
+ * kMaxKeyBytes) */
+__host__ __device__ inline uint64_t desc_pack(uint32_t tag, uint32_t mode, uint32_t nkeys, uint32_t nbytes)
 {
-    return ((uint64_t)(seq + 1u) << 32) | (uint64_t)(mode & 15u) | ((uint64_t)(nkeys & 0xfffu) << 4) |
+    return ((uint64_t)tag << 32) | (uint64_t)(mode & 15u) | ((uint64_t)(nkeys & 0xfffu) << 4) |
            ((uint64_t)(nbytes & 0xffffu) << 16);
 }
 static_assert(kMaxKeys <= 0xfffu && kMaxKeyBytes <= 0xffffu, "descriptor fields");
 
-__device__ __forceinline__ uint32_t ld_sys(const uint32_t *p)
+__device__ __forceinline__ uint32_t ld_rlx(const uint32_t *p)
 {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ uint64_t ld_rlx64(const uint64_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ void st_sys(uint32_t *p, uint32_t v)
@@ -91,57 +124,122 @@ __device__ __forceinline__ void st_sys(uint32_t *p, uint32_t v)
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p)
+__device__ __forceinline__ void st_sys64(uint64_t *p, uint64_t v)
 {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+/* a system-scope release whose write-back is waited for: hipcc (ROCm 7.2,
+ * gfx950) drops the fence's vmcnt(0) after its L2 write-back when the
+ * scoreboard looks empty (MI355X_MICROARCH.md), so wait explicitly */
+__device__ __forceinline__ void release_sys()
+{
+    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 __device__ __forceinline__ uint64_t ticks() { return wall_clock64(); } /* s_memrealtime, 100 MHz */
 
-/* the worker of one lane: its batches are seq = lseq * nlanes + lane for
- * lseq = start, start + 1, ... (ctl is the lane's control block) */
-__global__ __launch_bounds__(kThreads) void nc_ring_worker(RingCtl *ctl, const uint64_t *desc, uint32_t *done,
-                                                          const uint32_t *offs, const uint8_t *keys, uint32_t *outs,
-                                                          uint32_t nslots, uint32_t max_keys, uint64_t kstride,
-                                                          uint32_t lseq, uint32_t lane, uint32_t nlanes)
+/* the batch's keys, thread t taking keys t, t + T, ...: each read from the
+ * LDS image by the realigning reader (which may read up to 22 bytes past a
+ * key: the image's NC_GPUHASH_PAD tail) */
+template <int MODE, uint32_t T>
+__device__ __forceinline__ void serve(const LdsSrc &src, const uint32_t *loff, uint32_t nk, const uint32_t *tab,
+                                      uint32_t *so_out)
+{
+    for (uint32_t i = threadIdx.x; i < nk; i += T) {
+        const uint32_t sp = loff[i]; /* start | end << 16 in the image */
+        so_out[i] = hash_key<MODE, 0>(src, sp & 0xffffu, (sp >> 16) - (sp & 0xffffu), tab);
+    }
+}
+
+/* one poll of a lane's next slot: three relaxed loads issued together */
+struct Poll {
+    uint64_t d;
+    uint32_t stop, closing;
+    __device__ __forceinline__ void issue(RingCtl *c, const uint64_t *dp, RingDev *dv)
+    {
+        stop = ld_rlx(&c->stop);
+        d = ld_rlx64(dp);
+        closing = __hip_atomic_load(&dv->closing, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+};
+
+/* thread 0: a poll's outcome. 1: stop (go = 0) or the batch is published (go
+ * = 1, lo = the descriptor's low word) or, once leaving, nothing came (go =
+ * 0); -1: the launch is ending and `exiting` was just published (poll once
+ * more); 0: keep polling. The idle and life limits as in the file comment. */
+__device__ __forceinline__ int poll_check(const Poll &p, uint32_t tag, uint32_t epoch, uint64_t born, uint64_t &last,
+                                          bool &leaving, RingCtl *c, RingDev *dv, uint32_t &go, uint32_t &lo)
+{
+    if (p.stop != 0u) return 1;
+    if ((uint32_t)(p.d >> 32) == tag) { /* published: the shape came with it */
+        go = 1;
+        lo = (uint32_t)p.d;
+        return 1;
+    }
+    if (leaving) return 1; /* the descriptor was re-read after `exiting`: the host relaunches */
+    const uint64_t now = ticks();
+    bool close = p.closing == epoch;
+    if (!close && now - born > kLifeTicks) close = true;
+    if (!close && now - last > kIdleTicks) {
+        const uint64_t any = __hip_atomic_load(&dv->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        close = now > any && now - any > kIdleTicks;
+        if (!close) last = any;
+    }
+    if (!close) return 0;
+    __hip_atomic_store(&dv->closing, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_sys(&c->exiting, 1u);
+    release_sys();
+    leaving = true;
+    return -1;
+}
+
+/* one launch, one workgroup per lane (lane = blockIdx.x): lane g's batches
+ * are seq = k * nlanes + g for k = processed, processed + 1, ... */
+template <uint32_t T>
+__global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, const uint64_t *desc, uint32_t *done,
+                                                    const uint32_t *offs, const uint8_t *keys, uint32_t *outs,
+                                                    uint32_t nslots, uint32_t max_keys, uint64_t kstride,
+                                                    uint32_t nlanes, uint32_t epoch, uint64_t *tl)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
     __shared__ uint32_t crc16t[256], crc32t[256];
     __shared__ uint32_t cmd[2]; /* go, the descriptor's low word */
-    const uint32_t t = threadIdx.x;
+    const uint32_t t = threadIdx.x, lane = blockIdx.x;
+    RingCtl *c = ctl + lane;
     uint32_t *loff = reinterpret_cast<uint32_t *>(dyn);
     uint8_t *lkeys = dyn + ((4u * (max_keys + 1u) + 15u) & ~15u);
-    for (uint32_t i = t; i < 256u; i += kThreads) {
+    for (uint32_t i = t; i < 256u; i += T) {
         crc16t[i] = nc_crc16_entry(i);
         crc32t[i] = nc_crc32_entry(i);
     }
+    /* where this lane resumes: its next batch's slot and tag, carried forward
+     * by nlanes per batch (mod nslots, mod 2^31) */
+    uint64_t done_count = __hip_atomic_load(&c->processed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t seq0 = done_count * nlanes + lane;
+    uint32_t s = (uint32_t)(seq0 % nslots), tag = ring_tag(seq0);
     const uint64_t born = ticks();
     uint64_t last = born;
+    bool leaving = false; /* thread 0: `exiting` published and fenced */
+    uint64_t t_found = 0, t_staged = 0, t_issued = 0; /* thread 0: the diagnostic timeline (tl) */
     for (;;) {
-        const uint32_t seq = lseq * nlanes + lane, s = seq % nslots;
         if (t == 0u) {
             uint32_t go = 0, lo = 0;
+            /* one poll at a time: the acquire fence after a match waits for
+             * every load in flight, so a second poll in flight (issued half a
+             * round trip later) costs the batch more than it saves
+             * (measured: depth 1 7.3-7.9 -> 8.1-8.7 us) */
             for (;;) {
-                if (ld_sys(&ctl->stop) != 0u) break;
-                const uint64_t d = ld_sys64(desc + s);
-                if ((uint32_t)(d >> 32) == seq + 1u) { /* published: the shape came with it */
-                    go = 1;
-                    lo = (uint32_t)d;
-                    break;
-                }
-                const uint64_t now = ticks();
-                if (now - last > kIdleTicks || now - born > kLifeTicks) {
-                    st_sys(&ctl->exiting, 1u);
-                    __threadfence_system();
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* MI355X_MICROARCH.md: the fence's own wait may be dropped */
-                    if ((uint32_t)(ld_sys64(desc + s) >> 32) == seq + 1u && now - born <= kLifeTicks) {
-                        st_sys(&ctl->exiting, 0u); /* a batch arrived meanwhile: stay */
-                        last = now;
-                        continue;
-                    }
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
+                Poll p;
+                p.issue(c, desc + s, dv);
+                const int r = poll_check(p, tag, epoch, born, last, leaving, c, dv, go, lo);
+                if (r > 0) break;
+                if (r == 0) __builtin_amdgcn_s_sleep(2);
+            }
+            if (go) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); /* system scope: the staging's bytes after the descriptor */
+                t_found = ticks();
             }
             cmd[0] = go;
             cmd[1] = lo;
@@ -157,41 +255,73 @@ __global__ __launch_bounds__(kThreads) void nc_ring_worker(RingCtl *ctl, const u
         const uint32_t *so = offs + (uint64_t)s * max_keys;
         const u32x4 *sk = reinterpret_cast<const u32x4 *>(keys + (uint64_t)s * kstride);
         const uint32_t nq = (nb + 15u) / 16u;
-        uint32_t ov[(kMaxKeys + kThreads - 1u) / kThreads];
-        u32x4 kv[(kMaxKeyBytes / 16u + kThreads - 1u) / kThreads];
+        uint32_t ov[(kMaxKeys + T - 1u) / T];
+        u32x4 kv[(kMaxKeyBytes / 16u + T - 1u) / T];
 #pragma unroll
         for (uint32_t j = 0; j < sizeof(ov) / sizeof(ov[0]); j++)
-            if (t + j * kThreads < nk) ov[j] = __builtin_nontemporal_load(so + t + j * kThreads);
+            if (t + j * T < nk) ov[j] = __builtin_nontemporal_load(so + t + j * T);
 #pragma unroll
         for (uint32_t j = 0; j < sizeof(kv) / sizeof(kv[0]); j++)
-            if (t + j * kThreads < nq) kv[j] = __builtin_nontemporal_load(sk + t + j * kThreads);
+            if (t + j * T < nq) kv[j] = __builtin_nontemporal_load(sk + t + j * T);
 #pragma unroll
         for (uint32_t j = 0; j < sizeof(ov) / sizeof(ov[0]); j++)
-            if (t + j * kThreads < nk) loff[t + j * kThreads] = ov[j];
+            if (t + j * T < nk) loff[t + j * T] = ov[j];
 #pragma unroll
         for (uint32_t j = 0; j < sizeof(kv) / sizeof(kv[0]); j++)
-            if (t + j * kThreads < nq) reinterpret_cast<u32x4 *>(lkeys)[t + j * kThreads] = kv[j];
+            if (t + j * T < nq) reinterpret_cast<u32x4 *>(lkeys)[t + j * T] = kv[j];
         __syncthreads();
+        if (tl != nullptr && t == 0u) t_staged = ticks();
         uint32_t *so_out = outs + (uint64_t)s * max_keys;
-        for (uint32_t i = t; i < nk; i += kThreads) {
-            const uint32_t sp = loff[i]; /* start | end << 16 in the image */
-            so_out[i] = nc_key_hash((int)mode, lkeys + (sp & 0xffffu), (sp >> 16) - (sp & 0xffffu), crc16t, crc32t);
+        const LdsSrc src{reinterpret_cast<const uint32_t *>(lkeys)};
+        switch (mode) {
+        case NC_GPUHASH_ONE_AT_A_TIME: serve<NC_GPUHASH_ONE_AT_A_TIME, T>(src, loff, nk, crc32t, so_out); break;
+        case NC_GPUHASH_MD5: serve<NC_GPUHASH_MD5, T>(src, loff, nk, crc32t, so_out); break;
+        case NC_GPUHASH_CRC16: serve<NC_GPUHASH_CRC16, T>(src, loff, nk, crc16t, so_out); break;
+        case NC_GPUHASH_CRC32: serve<NC_GPUHASH_CRC32, T>(src, loff, nk, crc32t, so_out); break;
+        case NC_GPUHASH_CRC32A: serve<NC_GPUHASH_CRC32A, T>(src, loff, nk, crc32t, so_out); break;
+        case NC_GPUHASH_FNV1_64: serve<NC_GPUHASH_FNV1_64, T>(src, loff, nk, crc32t, so_out); break;
+        case NC_GPUHASH_FNV1A_64: serve<NC_GPUHASH_FNV1A_64, T>(src, loff, nk, crc32t, so_out); break;
+        case NC_GPUHASH_FNV1_32: serve<NC_GPUHASH_FNV1_32, T>(src, loff, nk, crc32t, so_out); break;
+        case NC_GPUHASH_FNV1A_32: serve<NC_GPUHASH_FNV1A_32, T>(src, loff, nk, crc32t, so_out); break;
+        case NC_GPUHASH_HSIEH: serve<NC_GPUHASH_HSIEH, T>(src, loff, nk, crc32t, so_out); break;
+        case NC_GPUHASH_MURMUR: serve<NC_GPUHASH_MURMUR, T>(src, loff, nk, crc32t, so_out); break;
+        default: serve<NC_GPUHASH_JENKINS, T>(src, loff, nk, crc32t, so_out); break;
+        }
+        if (tl != nullptr) { /* diagnostics: every thread's hashes issued (stores not yet acknowledged) */
+            __syncthreads();
+            if (t == 0u) t_issued = ticks();
         }
         __builtin_amdgcn_s_waitcnt(0); /* this thread's hash stores acknowledged ... */
         __syncthreads();                /* ... in every wave ... */
+        done_count++;
         if (t == 0u) { /* ... then one system-scope release for the workgroup before the slot reads as done */
-            __threadfence_system();
-            /* hipcc (ROCm 7.2, gfx950) drops the fence's vmcnt(0) after its
-             * L2 write-back when the scoreboard looks empty, as it does after
-             * the s_waitcnt above (MI355X_MICROARCH.md): wait explicitly */
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            st_sys(&ctl->processed, lseq + 1u);
-            st_sys(&done[s], seq + 1u);
+            if (tl != nullptr) { /* found, staged, issued, stored: covered by the release below */
+                tl[8 * s + 0] = t_found;
+                tl[8 * s + 1] = t_staged;
+                tl[8 * s + 2] = t_issued;
+                tl[8 * s + 3] = ticks();
+            }
+            release_sys();
+            /* relaxed stores after the fence: a release store would wait for
+             * the write-back again. `processed` is read by the host only
+             * once the launch has ended */
+            __hip_atomic_store(&done[s], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&c->processed, done_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            last = ticks();
+            __hip_atomic_fetch_max(&dv->last, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tl != nullptr) { /* released; visible with the next batch's release */
+                tl[8 * s + 4] = last;
+                tl[8 * s + 5] = done_count;
+            }
         }
-        last = ticks();
-        lseq++;
+        tag = kTagBit | ((tag + nlanes) & kTagMask);
+        s += nlanes;
+        if (s >= nslots) s -= nslots; /* nlanes <= nslots */
     }
 }
+
+typedef void (*worker_fn)(RingCtl *, RingDev *, const uint64_t *, uint32_t *, const uint32_t *, const uint8_t *,
+                          uint32_t *, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t, uint64_t *);
 
 enum { SLOT_FREE = 0, SLOT_RUNNING = 1 };
 
@@ -199,20 +329,25 @@ enum { SLOT_FREE = 0, SLOT_RUNNING = 1 };
 
 struct nc_gpuhash_ring {
     int device;
-    uint32_t nslots, max_keys;
+    uint32_t nslots, max_keys, nlanes, threads;
     uint64_t max_key_bytes, kstride;
-    uint8_t *host; /* one mapped, coherent allocation: ctl[kLanes], desc, done, offsets, keys, outputs */
+    uint8_t *host; /* one mapped, coherent allocation: ctl[kMaxLanes], desc, done, offsets, keys, outputs */
     RingCtl *ctl, *d_ctl; /* one per lane */
     uint64_t *desc, *d_desc;
     uint32_t *done, *d_done, *offs, *d_offs, *outs, *d_outs;
     uint8_t *keys, *d_keys;
-    uint32_t nlanes;
-    hipStream_t stream[kLanes];
-    hipEvent_t ev[kLanes];
-    int launched[kLanes];
-    uint32_t lseq[kLanes]; /* per lane: batches submitted */
-    uint32_t seq;          /* next batch's sequence number */
-    uint32_t *slot_state, *slot_ticket, *slot_nkeys;
+    RingDev *dv; /* device memory */
+    hipStream_t stream;
+    hipEvent_t ev;
+    int launched;
+    int hold; /* diagnostics: no launch while set */
+    uint32_t epoch;
+    uint64_t seq;  /* next batch's sequence number */
+    uint64_t seq0; /* the first one this ring numbered */
+    uint64_t *tl, *d_tl; /* diagnostics: 8 words of device timeline per slot */
+    int timeline;
+    uint32_t *slot_state, *slot_nkeys;
+    uint64_t *slot_seq;
     uint32_t **slot_out;
     uint64_t launches;
     pthread_mutex_t lock;
@@ -224,38 +359,60 @@ static rstatus_t ring_fail(hipError_t e)
     return errno == ENOMEM ? NC_ENOMEM : NC_ERROR;
 }
 
+/* the LDS of a lane: span words, the key image, and 96 bytes for the
+ * realigning reader's look-ahead (md5's final block reads up to 86 bytes past
+ * its start, nc_lds_hash.h) */
 static size_t ring_lds(const nc_gpuhash_ring_t *r)
 {
-    return ((4u * (r->max_keys + 1u) + 15u) & ~(size_t)15u) + r->kstride;
+    return ((4u * (r->max_keys + 1u) + 15u) & ~(size_t)15u) + r->kstride + 96u;
+}
+
+static worker_fn ring_kernel(uint32_t threads)
+{
+    switch (threads) {
+    case 256: return nc_ring_worker<256>;
+    case 512: return nc_ring_worker<512>;
+    default: return nc_ring_worker<1024>;
+    }
+}
+
+/* lane g's batches numbered below r->seq (its lane-local submit count) */
+static inline uint64_t lane_submitted(const nc_gpuhash_ring_t *r, uint32_t g)
+{
+    return (r->seq + r->nlanes - 1u - g) / r->nlanes;
 }
 
 /* the key spans of a slot: start | end << 16, bytes in the staged image */
 static inline uint32_t span_word(uint64_t a, uint64_t b) { return (uint32_t)a | ((uint32_t)b << 16); }
 
-/* lock held: lane g's worker is running, or one is launched from the lane's
+/* lock held: lane g's worker is running and will see its published batches,
+ * or the launch has ended and a new one starts every lane at its
  * `processed` */
 static rstatus_t ring_ensure_worker(nc_gpuhash_ring_t *r, uint32_t g)
 {
-    RingCtl *c = r->ctl + g;
-    if (r->launched[g]) {
-        if (__atomic_load_n(&c->exiting, __ATOMIC_ACQUIRE) == 0u) return NC_OK; /* alive: it sees the descriptor */
-        const hipError_t q = hipEventQuery(r->ev[g]);
+    if (r->launched) {
+        if (__atomic_load_n(&r->ctl[g].exiting, __ATOMIC_ACQUIRE) == 0u) return NC_OK; /* alive: it sees the descriptor */
+        const hipError_t q = hipEventQuery(r->ev);
         if (q == hipErrorNotReady) return NC_OK; /* still leaving: relaunch on a later poll */
         if (q != hipSuccess) return ring_fail(q);
+        r->launched = 0;
     }
-    const uint32_t start = __atomic_load_n(&c->processed, __ATOMIC_ACQUIRE);
-    if (start == r->lseq[g] && r->launched[g]) return NC_OK; /* nothing to do */
-    __atomic_store_n(&c->exiting, 0u, __ATOMIC_SEQ_CST);
+    int pending = 0;
+    for (uint32_t h = 0; h < r->nlanes; h++)
+        pending |= __atomic_load_n(&r->ctl[h].processed, __ATOMIC_ACQUIRE) != lane_submitted(r, h);
+    if (!pending || r->hold) return NC_OK;
+    for (uint32_t h = 0; h < r->nlanes; h++) __atomic_store_n(&r->ctl[h].exiting, 0u, __ATOMIC_SEQ_CST);
     hipError_t e = hipSetDevice(r->device);
     if (e != hipSuccess) return ring_fail(e);
     (void)hipGetLastError();
-    hipLaunchKernelGGL(nc_ring_worker, dim3(1), dim3(kThreads), ring_lds(r), r->stream[g], r->d_ctl + g, r->d_desc,
-                       r->d_done, r->d_offs, r->d_keys, r->d_outs, r->nslots, r->max_keys, r->kstride, start, g,
-                       r->nlanes);
+    r->epoch++;
+    hipLaunchKernelGGL(ring_kernel(r->threads), dim3(r->nlanes), dim3(r->threads), ring_lds(r), r->stream, r->d_ctl,
+                       r->dv, r->d_desc, r->d_done, r->d_offs, r->d_keys, r->d_outs, r->nslots, r->max_keys,
+                       r->kstride, r->nlanes, r->epoch, r->timeline ? r->d_tl : nullptr);
     e = hipGetLastError();
-    if (e == hipSuccess) e = hipEventRecord(r->ev[g], r->stream[g]);
+    if (e == hipSuccess) e = hipEventRecord(r->ev, r->stream);
     if (e != hipSuccess) return ring_fail(e);
-    r->launched[g] = 1;
+    r->launched = 1;
     r->launches++;
     return NC_OK;
 }
@@ -263,27 +420,27 @@ static rstatus_t ring_ensure_worker(nc_gpuhash_ring_t *r, uint32_t g)
 extern "C" void nc_gpuhash_ring_destroy(nc_gpuhash_ring_t *r)
 {
     if (r == NULL) return;
-    for (uint32_t g = 0; g < kLanes && r->ctl != NULL; g++) __atomic_store_n(&r->ctl[g].stop, 1u, __ATOMIC_SEQ_CST);
+    for (uint32_t g = 0; g < kMaxLanes && r->ctl != NULL; g++) __atomic_store_n(&r->ctl[g].stop, 1u, __ATOMIC_SEQ_CST);
     (void)hipSetDevice(r->device);
-    for (uint32_t g = 0; g < kLanes; g++) {
-        if (r->launched[g]) (void)hipEventSynchronize(r->ev[g]); /* the worker returns at its next poll */
-        if (r->ev[g]) (void)hipEventDestroy(r->ev[g]);
-        if (r->stream[g]) (void)hipStreamDestroy(r->stream[g]);
-    }
+    if (r->launched) (void)hipEventSynchronize(r->ev); /* every lane returns at its next poll */
+    if (r->ev) (void)hipEventDestroy(r->ev);
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    if (r->dv) (void)hipFree(r->dv);
     if (r->host) (void)hipHostFree(r->host);
     free(r->slot_state);
-    free(r->slot_ticket);
+    free(r->slot_seq);
     free(r->slot_nkeys);
     free(r->slot_out);
     pthread_mutex_destroy(&r->lock);
     free(r);
 }
 
-extern "C" nc_gpuhash_ring_t *nc_gpuhash_ring_create(int device, uint32_t nslots, uint32_t max_keys,
-                                                     uint64_t max_key_bytes)
+extern "C" nc_gpuhash_ring_t *nc_gpuhash_ring_create_ex(int device, uint32_t nslots, uint32_t max_keys,
+                                                        uint64_t max_key_bytes, uint32_t nlanes, uint32_t threads)
 {
     if (nslots == 0 || nslots > 1024 || max_keys == 0 || max_keys > kMaxKeys || max_key_bytes == 0 ||
-        max_key_bytes > kMaxKeyBytes) {
+        max_key_bytes > kMaxKeyBytes || nlanes > kMaxLanes ||
+        (threads != 0 && threads != 256 && threads != 512 && threads != 1024)) {
         errno = EINVAL;
         return NULL;
     }
@@ -299,28 +456,31 @@ extern "C" nc_gpuhash_ring_t *nc_gpuhash_ring_create(int device, uint32_t nslots
     pthread_mutex_init(&r->lock, NULL);
     r->device = device;
     r->nslots = nslots;
-    r->nlanes = nslots < kLanes ? 1u : kLanes;
+    if (nlanes == 0) nlanes = NC_GPUHASH_RING_DEFAULT_LANES;
+    r->nlanes = nlanes < nslots ? nlanes : nslots;
+    r->threads = threads ? threads : NC_GPUHASH_RING_DEFAULT_THREADS;
     r->max_keys = max_keys;
     r->max_key_bytes = max_key_bytes;
     r->kstride = (max_key_bytes + NC_GPUHASH_PAD + 15u) & ~15ull;
     r->slot_state = (uint32_t *)calloc(nslots, sizeof(uint32_t));
-    r->slot_ticket = (uint32_t *)calloc(nslots, sizeof(uint32_t));
+    r->slot_seq = (uint64_t *)calloc(nslots, sizeof(uint64_t));
     r->slot_nkeys = (uint32_t *)calloc(nslots, sizeof(uint32_t));
     r->slot_out = (uint32_t **)calloc(nslots, sizeof(uint32_t *));
-    const size_t o_ctl = 0, o_desc = sizeof(RingCtl) * kLanes, o_done = o_desc + 8u * nslots,
+    const size_t o_ctl = 0, o_desc = sizeof(RingCtl) * kMaxLanes, o_done = o_desc + 8u * nslots,
                  o_offs = (o_done + 4u * nslots + 127u) & ~(size_t)127u,
                  o_keys = (o_offs + 4ull * max_keys * nslots + 127u) & ~(size_t)127u,
-                 o_outs = o_keys + r->kstride * nslots, total = o_outs + 4ull * max_keys * nslots;
-    hipError_t e = r->slot_state && r->slot_ticket && r->slot_nkeys && r->slot_out ? hipSetDevice(device)
-                                                                                    : hipErrorOutOfMemory;
+                 o_outs = o_keys + r->kstride * nslots, o_tl = (o_outs + 4ull * max_keys * nslots + 127u) & ~(size_t)127u,
+                 total = o_tl + 64ull * nslots;
+    hipError_t e = r->slot_state && r->slot_seq && r->slot_nkeys && r->slot_out ? hipSetDevice(device)
+                                                                                : hipErrorOutOfMemory;
     if (e == hipSuccess) e = hipHostMalloc((void **)&r->host, total, hipHostMallocMapped | hipHostMallocCoherent);
     uint8_t *dev = NULL;
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&dev, r->host, 0);
-    for (uint32_t g = 0; g < r->nlanes; g++) {
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->stream[g], hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev[g], hipEventDisableTiming);
-    }
-    if (e == hipSuccess && (size_t)(4u * (max_keys + 1u) + r->kstride) > 64u * 1024u) e = hipErrorInvalidValue;
+    if (e == hipSuccess) e = hipMalloc((void **)&r->dv, sizeof(RingDev));
+    if (e == hipSuccess) e = hipMemset(r->dv, 0, sizeof(RingDev));
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev, hipEventDisableTiming);
+    if (e == hipSuccess && ring_lds(r) > 64u * 1024u) e = hipErrorInvalidValue;
     if (e != hipSuccess) {
         ring_fail(e);
         const int saved = errno;
@@ -335,6 +495,8 @@ extern "C" nc_gpuhash_ring_t *nc_gpuhash_ring_create(int device, uint32_t nslots
     r->offs = (uint32_t *)(r->host + o_offs);
     r->keys = r->host + o_keys;
     r->outs = (uint32_t *)(r->host + o_outs);
+    r->tl = (uint64_t *)(r->host + o_tl);
+    r->d_tl = (uint64_t *)(dev + o_tl);
     r->d_ctl = (RingCtl *)(dev + o_ctl);
     r->d_desc = (uint64_t *)(dev + o_desc);
     r->d_done = (uint32_t *)(dev + o_done);
@@ -344,11 +506,17 @@ extern "C" nc_gpuhash_ring_t *nc_gpuhash_ring_create(int device, uint32_t nslots
     return r;
 }
 
+extern "C" nc_gpuhash_ring_t *nc_gpuhash_ring_create(int device, uint32_t nslots, uint32_t max_keys,
+                                                     uint64_t max_key_bytes)
+{
+    return nc_gpuhash_ring_create_ex(device, nslots, max_keys, max_key_bytes, 0, 0);
+}
+
 /* lock held: deliver slot s if its batch is done; 1 when the slot is free */
 static int ring_reap(nc_gpuhash_ring_t *r, uint32_t s)
 {
     if (r->slot_state[s] == SLOT_FREE) return 1;
-    if (__atomic_load_n(&r->done[s], __ATOMIC_ACQUIRE) != r->slot_ticket[s] + 1u) return 0;
+    if (__atomic_load_n(&r->done[s], __ATOMIC_ACQUIRE) != ring_tag(r->slot_seq[s])) return 0;
     memcpy(r->slot_out[s], r->outs + (size_t)s * r->max_keys, (size_t)r->slot_nkeys[s] * sizeof(uint32_t));
     r->slot_state[s] = SLOT_FREE;
     return 1;
@@ -357,7 +525,7 @@ static int ring_reap(nc_gpuhash_ring_t *r, uint32_t s)
 extern "C" rstatus_t nc_gpuhash_ring_submit_spans(nc_gpuhash_ring_t *r, int mode, const struct nc_keyspan *spans,
                                                   uint32_t nkeys, uint32_t *out, int *ticket)
 {
-    if (r == NULL || (spans == NULL && nkeys) || out == NULL || ticket == NULL || mode < 0 ||
+    if (r == NULL || (spans == NULL && nkeys) || (out == NULL && nkeys) || ticket == NULL || mode < 0 ||
         mode >= NC_GPUHASH_NMODES) {
         errno = EINVAL;
         return NC_ERROR;
@@ -366,8 +534,26 @@ extern "C" rstatus_t nc_gpuhash_ring_submit_spans(nc_gpuhash_ring_t *r, int mode
         errno = ENOMEM;
         return NC_ENOMEM;
     }
+    /* the spans first, before any state changes: an inverted or NULL span is
+     * the caller's error */
+    const uint8_t *lo = nkeys ? spans[0].start : NULL, *hi = lo;
+    uint64_t klen = 0;
+    for (uint32_t i = 0; i < nkeys; i++) {
+        if (spans[i].start == NULL || spans[i].end < spans[i].start) {
+            errno = EINVAL;
+            return NC_ERROR;
+        }
+        if (spans[i].start < lo) lo = spans[i].start;
+        if (spans[i].end > hi) hi = spans[i].end;
+        klen += (uint64_t)(spans[i].end - spans[i].start);
+    }
+    if (klen > r->max_key_bytes) {
+        errno = ENOMEM;
+        return NC_ENOMEM;
+    }
     pthread_mutex_lock(&r->lock);
-    const uint32_t seq = r->seq, s = seq % r->nslots, g = seq % r->nlanes;
+    const uint64_t seq = r->seq;
+    const uint32_t s = (uint32_t)(seq % r->nslots), g = (uint32_t)(seq % r->nlanes);
     if (!ring_reap(r, s)) {
         pthread_mutex_unlock(&r->lock);
         errno = EAGAIN;
@@ -379,18 +565,6 @@ extern "C" rstatus_t nc_gpuhash_ring_submit_spans(nc_gpuhash_ring_t *r, int mode
      * mbuf), else key by key */
     uint8_t *kd = r->keys + (size_t)s * r->kstride;
     uint32_t *od = r->offs + (size_t)s * r->max_keys;
-    const uint8_t *lo = nkeys ? spans[0].start : NULL, *hi = lo;
-    uint64_t klen = 0;
-    for (uint32_t i = 0; i < nkeys; i++) {
-        if (spans[i].start < lo) lo = spans[i].start;
-        if (spans[i].end > hi) hi = spans[i].end;
-        klen += (uint64_t)(spans[i].end - spans[i].start);
-    }
-    if (klen > r->max_key_bytes) {
-        pthread_mutex_unlock(&r->lock);
-        errno = ENOMEM;
-        return NC_ENOMEM;
-    }
     uint64_t pos;
     if ((uint64_t)(hi - lo) <= r->max_key_bytes) {
         pos = (uint64_t)(hi - lo);
@@ -406,18 +580,16 @@ extern "C" rstatus_t nc_gpuhash_ring_submit_spans(nc_gpuhash_ring_t *r, int mode
         }
     }
     r->slot_state[s] = SLOT_RUNNING;
-    r->slot_ticket[s] = seq;
+    r->slot_seq[s] = seq;
     r->slot_nkeys[s] = nkeys;
     r->slot_out[s] = out;
     r->seq = seq + 1u;
-    r->lseq[g]++;
     /* every staging write before the descriptor; then `exiting`
      * (ring_ensure_worker) after it: the host's half of the leave protocol */
-    __atomic_store_n(&r->desc[s], desc_pack(seq, (uint32_t)mode, nkeys, (uint32_t)pos), __ATOMIC_SEQ_CST);
-    __atomic_store_n(&r->ctl[g].head, r->lseq[g], __ATOMIC_RELAXED);
+    __atomic_store_n(&r->desc[s], desc_pack(ring_tag(seq), (uint32_t)mode, nkeys, (uint32_t)pos), __ATOMIC_SEQ_CST);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
     const rstatus_t rc = ring_ensure_worker(r, g);
-    if (rc == NC_OK) *ticket = (int)(seq & 0x7fffffffu);
+    if (rc == NC_OK) *ticket = (int)(seq & kTagMask);
     pthread_mutex_unlock(&r->lock);
     return rc;
 }
@@ -429,15 +601,24 @@ extern "C" rstatus_t nc_gpuhash_ring_poll(nc_gpuhash_ring_t *r, int ticket)
         return NC_ERROR;
     }
     pthread_mutex_lock(&r->lock);
-    const uint32_t s = (uint32_t)ticket % r->nslots;
+    /* the ticket's batch: the latest seq below r->seq with these 31 bits */
+    const uint64_t back = (r->seq - (uint64_t)ticket) & kTagMask;
     rstatus_t rc = NC_OK;
-    if (r->slot_state[s] == SLOT_RUNNING && r->slot_ticket[s] == (uint32_t)ticket && !ring_reap(r, s)) {
-        rc = ring_ensure_worker(r, (uint32_t)ticket % r->nlanes); /* a worker that left while this batch came in is relaunched */
-        if (rc == NC_OK) {
-            errno = EAGAIN;
-            rc = NC_EAGAIN;
+    if (back == 0 || back > r->seq - r->seq0) { /* never issued */
+        errno = EINVAL;
+        rc = NC_ERROR;
+    } else if (back <= r->nslots) { /* one of the last nslots batches: its slot holds it or delivered it */
+        const uint64_t seq = r->seq - back;
+        const uint32_t s = (uint32_t)(seq % r->nslots);
+        if (r->slot_seq[s] == seq && r->slot_state[s] == SLOT_RUNNING && !ring_reap(r, s)) {
+            /* a lane whose worker left while this batch came in is relaunched */
+            rc = ring_ensure_worker(r, (uint32_t)(seq % r->nlanes));
+            if (rc == NC_OK) {
+                errno = EAGAIN;
+                rc = NC_EAGAIN;
+            }
         }
-    }
+    } /* older: its slot was reused, which delivered it first (ring_reap) */
     pthread_mutex_unlock(&r->lock);
     return rc;
 }
@@ -451,7 +632,7 @@ extern "C" rstatus_t nc_gpuhash_ring_wait(nc_gpuhash_ring_t *r, int ticket)
         if (rc != NC_EAGAIN) return rc;
         if ((spins & 1023u) == 1023u) {
             clock_gettime(CLOCK_MONOTONIC, &t1);
-            if (t1.tv_sec - t0.tv_sec > 10) { /* a worker ends within 2 s; this is a dead device */
+            if (t1.tv_sec - t0.tv_sec > 10) { /* a launch ends within 2 s; this is a dead device */
                 errno = EIO;
                 return NC_ERROR;
             }
@@ -461,3 +642,56 @@ extern "C" rstatus_t nc_gpuhash_ring_wait(nc_gpuhash_ring_t *r, int ticket)
 }
 
 extern "C" uint64_t nc_gpuhash_ring_launches(const nc_gpuhash_ring_t *r) { return r ? r->launches : 0; }
+
+extern "C" rstatus_t nc_gpuhash_ring_debug_start_seq(nc_gpuhash_ring_t *r, uint64_t seq)
+{
+    if (r == NULL) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    pthread_mutex_lock(&r->lock);
+    const int fresh = r->launches == 0 && r->seq == r->seq0;
+    if (fresh) {
+        r->seq = r->seq0 = seq;
+        for (uint32_t g = 0; g < r->nlanes; g++) __atomic_store_n(&r->ctl[g].processed, lane_submitted(r, g), __ATOMIC_SEQ_CST);
+    }
+    pthread_mutex_unlock(&r->lock);
+    if (!fresh) {
+        errno = EBUSY;
+        return NC_ERROR;
+    }
+    return NC_OK;
+}
+
+extern "C" rstatus_t nc_gpuhash_ring_debug_hold(nc_gpuhash_ring_t *r, int hold)
+{
+    if (r == NULL) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    pthread_mutex_lock(&r->lock);
+    r->hold = hold != 0;
+    pthread_mutex_unlock(&r->lock);
+    return NC_OK;
+}
+
+extern "C" uint32_t nc_gpuhash_ring_lanes(const nc_gpuhash_ring_t *r) { return r ? r->nlanes : 0; }
+
+extern "C" rstatus_t nc_gpuhash_ring_debug_timeline(nc_gpuhash_ring_t *r, int on, uint32_t slot, uint64_t out[8])
+{
+    if (r == NULL || (out != NULL && slot >= r->nslots)) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    pthread_mutex_lock(&r->lock);
+    const int ok = on < 0 || r->launches == 0 || r->timeline == (on != 0);
+    if (on >= 0 && ok) r->timeline = on != 0;
+    if (out != NULL)
+        for (int i = 0; i < 8; i++) out[i] = __atomic_load_n(&r->tl[8 * slot + i], __ATOMIC_ACQUIRE);
+    pthread_mutex_unlock(&r->lock);
+    if (!ok) {
+        errno = EBUSY;
+        return NC_ERROR;
+    }
+    return NC_OK;
+}

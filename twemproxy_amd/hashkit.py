@@ -534,19 +534,32 @@ class Context:
 
 
 class Ring:
-    """nc_gpuhash_ring: small batches (one mbuf's keys) served by resident
-    worker workgroups (one per lane, batch n on lane n % 2) that poll mapped
+    """nc_gpuhash_ring: small batches (one mbuf's keys) served by one resident
+    launch, one workgroup per lane (batch n on lane n % lanes), polling mapped
     host memory — no HIP call per batch (include/nc_gpuhash.h 3d). Tickets
     complete in order within a lane; poll each one. Thread-safe (the ring's
     mutex)."""
 
-    def __init__(self, device: int = 0, nslots: int = 4, max_keys: int = 4095, max_key_bytes: int = 32768):
+    def __init__(self, device: int = 0, nslots: int = 4, max_keys: int = 4095, max_key_bytes: int = 32768,
+                 lanes: int = 0, threads: int = 0):
         self._lib = L.lib()
-        handle = self._lib.nc_gpuhash_ring_create(device, nslots, max_keys, max_key_bytes)
+        handle = self._lib.nc_gpuhash_ring_create_ex(device, nslots, max_keys, max_key_bytes, lanes, threads)
         if not handle:
             raise L.NcError(ctypes.get_errno(), "nc_gpuhash_ring_create failed")
         self._h = handle
         self._keep: dict[int, tuple] = {}
+
+    @property
+    def lanes(self) -> int:
+        return int(self._lib.nc_gpuhash_ring_lanes(self._h))
+
+    def debug_start_seq(self, seq: int) -> None:
+        """number this (fresh) ring's batches from `seq` (tests of the ticket wrap)"""
+        L.check(self._lib.nc_gpuhash_ring_debug_start_seq(self._h, seq), "nc_gpuhash_ring_debug_start_seq")
+
+    def debug_hold(self, hold: bool) -> None:
+        """while held, no worker is launched: submitted batches stay pending"""
+        L.check(self._lib.nc_gpuhash_ring_debug_hold(self._h, int(hold)), "nc_gpuhash_ring_debug_hold")
 
     def close(self) -> None:
         if self._h:
