@@ -146,7 +146,8 @@ def test_auto_policy_choices():
     GSORT, CS, TK512, ISSUE = 1 << 25, 1 << 27, 1 << 26, 1 << 28
     n = 1 << 26
     assert t.pick_variant("fnv1a_64", n) == RS
-    assert t.pick_variant("md5", n) == DIRECT  # unknown shape
+    PADTAB = 1 << 15  # md5: padding selectors from the LDS table
+    assert t.pick_variant("md5", n) == DIRECT | PADTAB  # unknown shape
     # C2 (Zipf 8-64 B, mean 19.3)
     for name in ("fnv1a_64", "fnv1_64", "fnv1_32", "fnv1a_32"):  # six resident sets
         assert t.pick_variant(name, n, (19 * n, 8, 64)) == GSORT | CS | TK512, name
@@ -156,10 +157,10 @@ def test_auto_policy_choices():
     assert t.pick_variant("crc32", n, (19 * n, 8, 64)) == WG | OVER
     assert t.pick_variant("one_at_a_time", n, (19 * n, 8, 64)) == GSORT | CS | TK512 | ISSUE
     assert t.pick_variant("one_at_a_time", n, (21 * n, 8, 64)) == GSORT | CS | TK512 | ISSUE
-    assert t.pick_variant("md5", n, (19 * n, 8, 64)) == DIRECT
+    assert t.pick_variant("md5", n, (19 * n, 8, 64)) == DIRECT | PADTAB
     # uniform 8-64 B (mean 36)
     assert t.pick_variant("fnv1a_64", n, (36 * n, 8, 64)) == RS
-    assert t.pick_variant("md5", n, (36 * n, 8, 64)) == DIRECT
+    assert t.pick_variant("md5", n, (36 * n, 8, 64)) == DIRECT | PADTAB
     assert t.pick_variant("crc32a", n, (36 * n, 8, 64)) == RS | OVER
     # C3 (fixed 32 B)
     for name in ("fnv1_64", "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur"):
@@ -168,10 +169,10 @@ def test_auto_policy_choices():
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT | IL32, name
     for name in ("one_at_a_time", "jenkins"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == RS, name
-    assert t.pick_variant("md5", n, (32 * n, 32, 32)) == DIRECT
+    assert t.pick_variant("md5", n, (32 * n, 32, 32)) == DIRECT | PADTAB
     # short fixed, long keys (C4)
     assert t.pick_variant("fnv1a_64", n, (8 * n, 8, 8)) == WG
-    assert t.pick_variant("md5", n, (16 * n, 16, 16)) == DIRECT
+    assert t.pick_variant("md5", n, (16 * n, 16, 16)) == DIRECT | PADTAB
     for name in ("crc32", "one_at_a_time", "crc16"):
         assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | IL32, name
     for name in ("fnv1a_64", "fnv1_32"):  # eight-wave workgroups, one per CU

@@ -383,14 +383,15 @@ def test_wave_ring_crc_sliced(gpu, oracle, var):
 @pytest.mark.parametrize("var", [1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (8 << 20), (1 << 19) | (10 << 20),
                                  (1 << 19) | (11 << 20), (1 << 19) | (14 << 20), (1 << 19) | (9 << 20),
                                  (1 << 19) | (14 << 20) | (1 << 12), (1 << 19) | (10 << 20) | (1 << 13),
-                                 (1 << 19) | (14 << 20) | (1 << 13), (1 << 19) | (1 << 13)],
+                                 (1 << 19) | (14 << 20) | (1 << 13), (1 << 19) | (1 << 13), (1 << 19) | (1 << 15),
+                                 (1 << 19) | (8 << 20) | (1 << 15)],
                          ids=["direct", "lines", "il16", "il32", "il64", "lines_il32", "il8", "lines_il32_w8",
-                              "il32_s8", "lines_il32_s8", "direct_s8"])
+                              "il32_s8", "lines_il32_s8", "direct_s8", "direct_padtab", "il16_padtab"])
 def test_direct_ragged_tiles(gpu, oracle, var):
     """The direct per-lane pipelines (md5 and the byte-serial modes; the other
     modes take their default pipeline), consecutive or grid-interleaved tiles
     per wave, the byte modes' eight-wave line-image workgroups (bit 12), the
-    crcs' slicing-by-8 tables (bit 13), on
+    crcs' slicing-by-8 tables (bit 13), md5's LDS padding selectors (bit 15), on
     batch sizes around the 64-key tile and the per-workgroup tile
     count, with empty keys, one-block, multi-block and padding-only-block keys,
     a misaligned key buffer, against the oracle."""
@@ -459,7 +460,7 @@ def test_md5_fixed_length_specialisation(gpu, oracle, fl):
             keys, off = t.pack_keys(parts)
         kd, od = to_dev(keys, off, shift=5)
         want = oracle.batch(1, keys, off)
-        for var in (0, (1 << 19) | (1 << 26)):
+        for var in (0, (1 << 19) | (1 << 26), (1 << 19) | (1 << 15)):
             L.lib().nc_gpuhash_set_tuning(0, 0, var)
             try:
                 got = t.hash_batch_device("md5", kd, od, shape=(int(off[-1]), fl, fl))

@@ -1937,7 +1937,8 @@ constexpr int kVarNoPacked = 1 << 27; /* server_idx A/B: the 5-byte LDS continuu
 constexpr int kVarDirect8 = 1 << 12;     /* line image: eight-wave workgroups, one per CU */
 constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
 constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
-static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash) &
+constexpr int kVarMd5PadTab = 1 << 15;    /* md5: padding selectors from an LDS table */
+static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash | kVarMd5PadTab) &
                (kVarMd5Direct | (15 << 20) | kVarNoFixedLen | kVarWsort | kVarGsort | kVarNoPacked | (3 << 29))) == 0,
               "direct-pipeline options overlap the pipeline choice, its nibble or the server_idx bits");
 
@@ -2399,7 +2400,11 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
         /* ... with a wave's tiles interleaved over the grid (option bit 3):
          * C4 shard 1.822-1.857 -> 1.803-1.830 ms in two same-box A/Bs
          * (profiles/r04_lines_chunk_ab.jsonl, r04_crc_bytetable_ab.jsonl) */
-        return kVarMd5Direct | (lds ? (12 << 20) : 0);
+        /* ... and the per-lane padding selectors from the 512-byte LDS table
+         * (pad_block_tab): C2 SQ_INSTS_VALU 443 M -> 408 M per launch,
+         * 0.7319 -> 0.7259 and 0.7345 -> 0.7278 ms on two boxes
+         * (profiles/r05_md5_padtab_ab.jsonl, pmc_r05_md5pt.json) */
+        return kVarMd5Direct | (lds ? (12 << 20) : kVarMd5PadTab);
     }
     if (sh == nullptr || nkeys == 0 || sh->key_bytes == 0) return kVarRegStaged;
     const uint64_t mean = sh->key_bytes / nkeys;
@@ -2490,7 +2495,8 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
                                         (var & kVarNoFixedLen) == 0
                                     ? (uint32_t)shape->min_len
                                     : 0u;
-            return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15, fl);
+            return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream,
+                                  ((var >> 20) & 15) | ((var & kVarMd5PadTab) != 0 ? 16 : 0), fl);
         }
         if (nc_bytes::supports(mode))
             return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream,

@@ -148,13 +148,19 @@ __device__ __forceinline__ void flush_tails(uint32_t *qmem, uint32_t (*qmeta)[2]
  * key i = keys[off[i], off[i+1]); keys stays readable NC_GPUHASH_PAD bytes
  * past off[nkeys]. A tile of 64 keys spans less than 4 GiB.
  */
-template <bool LDS, bool IL, int FL = 0>
+template <bool LDS, bool IL, int FL = 0, bool PT = false>
 __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
                                                            uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
 {
     __shared__ uint32_t qmem[kWaves * kQWords * kQ];
     __shared__ uint32_t qmeta[kWaves][2];
+    /* PT: the padding selectors from a 512-byte LDS table (pad_block_tab) */
+    __shared__ uint32_t ptab[PT ? kPadTabWords : 1];
+    if constexpr (PT) {
+        for (uint32_t i = threadIdx.x; i < kPadTabWords; i += 256u) ptab[i] = pad_tab_entry(i);
+        __syncthreads();
+    }
     /* LDS: the next round's blocks arrive by LDS-DMA into a per-wave 4 KiB
      * image (key k's 64 bytes at k * 64) instead of into registers */
     __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? kWaves * kImage : 16];
@@ -218,7 +224,8 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                 cur[(FL / 4) >> 2][(FL / 4) & 3] = __builtin_amdgcn_perm(cur[(FL / 4) >> 2][(FL / 4) & 3], pad_src, bnd);
             }
         } else if (act) {
-            pad_block(cur, rem < 64 ? rem : 64, pad_src);
+            if constexpr (PT) pad_block_tab(cur, rem < 64 ? rem : 64, pad_src, ptab);
+            else pad_block(cur, rem < 64 ? rem : 64, pad_src);
             const bool fin = rem <= 55; /* the bit length fits behind the pad */
             if (fin) {
                 cur[3][2] = len << 3;
@@ -415,21 +422,23 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
 
 namespace nc_md5 {
 
-template <int FL>
+template <int FL, bool PT>
 void launch_fl(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
                uint64_t grid, uint64_t ntiles, uint32_t chunk)
 {
-    hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, FL>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
+    hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, FL, PT>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
                        d_off, nkeys, d_out, ntiles, chunk);
 }
 
 /* var: bits 0-1 tiles per wave (0: 16, 1: 8, 2: 32, 3: 64); bit 2: the LDS-DMA
- * variant (long keys); bit 3 tiles interleaved over the grid. fl: the batch's
+ * variant (long keys); bit 3 tiles interleaved over the grid; bit 4 the
+ * padding selectors from the LDS table (pad_block_tab). fl: the batch's
  * fixed key length if the caller's shape says so (0: unknown or varying);
  * 16, 20, 24, 32, 40 and 48 have specialised instantiations (each tile still
  * checks its lengths) */
-hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
-                  int var, uint32_t fl)
+template <bool PT>
+hipError_t launch_pt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
+                     hipStream_t stream, int var, uint32_t fl)
 {
     static const uint32_t kChunk[4] = {16, 8, 32, 64};
     const uint32_t chunk = kChunk[var & 3];
@@ -446,22 +455,29 @@ hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, 
             hipLaunchKernelGGL(nc_md5_lines_kernel<false>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off,
                                nkeys, d_out, ntiles, chunk);
     } else if (il) {
-        hipLaunchKernelGGL((nc_md5_direct_kernel<false, true>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
-                           d_off, nkeys, d_out, ntiles, chunk);
+        hipLaunchKernelGGL((nc_md5_direct_kernel<false, true, 0, PT>), dim3((unsigned)grid), dim3(256), 0, stream,
+                           d_keys, d_off, nkeys, d_out, ntiles, chunk);
     } else if (fl == 16 || fl == 20 || fl == 24 || fl == 32 || fl == 40 || fl == 48) {
         switch (fl) {
-        case 16: launch_fl<16>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
-        case 20: launch_fl<20>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
-        case 24: launch_fl<24>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
-        case 32: launch_fl<32>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
-        case 40: launch_fl<40>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
-        default: launch_fl<48>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        case 16: launch_fl<16, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        case 20: launch_fl<20, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        case 24: launch_fl<24, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        case 32: launch_fl<32, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        case 40: launch_fl<40, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
+        default: launch_fl<48, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
         }
     } else {
-        hipLaunchKernelGGL((nc_md5_direct_kernel<false, false>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
-                           d_off, nkeys, d_out, ntiles, chunk);
+        hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, 0, PT>), dim3((unsigned)grid), dim3(256), 0, stream,
+                           d_keys, d_off, nkeys, d_out, ntiles, chunk);
     }
     return hipGetLastError();
+}
+
+hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
+                  int var, uint32_t fl)
+{
+    return (var & 16) ? launch_pt<true>(d_keys, d_off, nkeys, d_out, stream, var, fl)
+                      : launch_pt<false>(d_keys, d_off, nkeys, d_out, stream, var, fl);
 }
 
 } // namespace nc_md5

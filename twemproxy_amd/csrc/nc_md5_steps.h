@@ -228,6 +228,38 @@ __device__ __forceinline__ void pad_block(md5_u32x4 (&d)[4], int32_t m, uint32_t
     for (int t = 0; t < 16; t++) d[t >> 2][t & 3] = pad_word(d[t >> 2][t & 3], y0 - t * kStep);
 }
 
+/* The selectors as a table (pad_block_tab): the selector of a word with d
+ * key bytes left from its start is kKeep for d >= 4, kBoundary[d] for d in
+ * 0..3 and 0 (every byte from kPadSrc's zero byte) for d < 0. Entry i holds
+ * d = 64 - i, so word t of a block holding m key bytes reads entry
+ * 64 - m + 4t: one per-lane base and the word's offset as the LDS read's
+ * immediate. 128 entries cover m = 1..64, t = 0..15. Lanes whose m differ by
+ * 28 or 32 meet in a bank (~3.5 conflict cycles per read on C2); a second
+ * copy 16 banks over for long keys moved the conflicts rather than removing
+ * them (57 values of m over 32 banks), profiles/pmc_r05_md5pt.json. */
+constexpr uint32_t kPadTabWords = 128;
+
+__device__ __forceinline__ uint32_t pad_tab_entry(uint32_t i)
+{
+    const int32_t d = 64 - (int32_t)i;
+    if (d >= 4) return (uint32_t)kKeep;
+    if (d < 0) return 0u;
+    return d == 0 ? kBoundary0 : (d == 1 ? kBoundary1 : (d == 2 ? kBoundary2 : kBoundary3));
+}
+
+/* pad_block with its selectors read from the LDS table gtab (eight
+ * ds_read2_b32 on the LDS pipe) instead of computed: one VALU per word (the
+ * perm) instead of three (the form's subtract, the clamp, the perm) */
+__device__ __forceinline__ void pad_block_tab(md5_u32x4 (&d)[4], int32_t m, uint32_t pad_src, const uint32_t *gtab)
+{
+    const uint32_t *g = gtab + (64 - m);
+    uint32_t sel[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) sel[t] = g[4 * t];
+#pragma unroll
+    for (int t = 0; t < 16; t++) d[t >> 2][t & 3] = __builtin_amdgcn_perm(d[t >> 2][t & 3], pad_src, sel[t]);
+}
+
 /* pad_block with the wave-uniform cases of msg_words (the line kernel, whose
  * blocks come from LDS reads, so no load is in flight into d): a length
  * shared by every lane pads by scalar selectors, a full block (m = 64 on
