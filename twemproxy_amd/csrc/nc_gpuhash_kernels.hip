@@ -2109,6 +2109,8 @@ hipError_t launch_gs_mode(const uint8_t *base, const uint64_t *off, uint64_t del
     const bool d3 = (var & (1 << 23)) != 0;
     if constexpr (MODE == NC_GPUHASH_FNV1A_64) {
         if (var & (1 << 20)) {
+            if ((var & kVarGsortCs) && (var & kVarGsort512))
+                return launch_gs<MODE, 8, 2, true, 512>(base, off, delta, nkeys, out, stream, var);
             if (var & kVarGsortCs) return launch_gs<MODE, 8, 2, true>(base, off, delta, nkeys, out, stream, var);
             return d3 ? launch_gs<MODE, 8, 3>(base, off, delta, nkeys, out, stream, var)
                       : launch_gs<MODE, 8, 2>(base, off, delta, nkeys, out, stream, var);
