@@ -135,7 +135,9 @@ def test_auto_policy_choices():
     the direct per-lane block pipeline (its LDS-DMA line image from 64-byte
     keys); the byte-serial modes on the direct pipeline for long keys (the
     fnvs in eight-wave workgroups) and the crcs for fixed short keys (tiles
-    interleaved over the grid, 32 per wave, for both); the register-staged workgroup pipeline when the
+    interleaved over the grid, 32 per wave, for both; crc32 / crc32a and
+    one_at_a_time on fixed 20-32 B keys through the eight-wave short-key
+    kernel); the register-staged workgroup pipeline when the
     shape is unknown; oversubscribed workgroup grids (and length grouping) for
     varying lengths; the wave ring for fixed 20-40 B fnv-like keys; the
     grouped workgroup pipeline (one length quartile per wave) on C2-like
@@ -165,10 +167,13 @@ def test_auto_policy_choices():
     # C3 (fixed 32 B)
     for name in ("fnv1_64", "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh", "murmur"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == RING5, name
-    for name in ("crc16", "crc32", "crc32a"):
-        assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT | IL32, name
-    for name in ("one_at_a_time", "jenkins"):
-        assert t.pick_variant(name, n, (32 * n, 32, 32)) == RS, name
+    SHORT = 1 << 11  # the short-key kernel (eight waves per CU); bits 20-21 depth, 22-23 the crc tables
+    assert t.pick_variant("crc16", n, (32 * n, 32, 32)) == DIRECT | IL32
+    for name in ("crc32", "crc32a"):  # three tiles in flight, slicing-by-8
+        assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT | SHORT | (2 << 20) | (1 << 22), name
+    assert t.pick_variant("one_at_a_time", n, (32 * n, 32, 32)) == DIRECT | SHORT | (2 << 20)
+    assert t.pick_variant("crc32", n, (36 * n, 36, 36)) == DIRECT | IL32  # longer than 32 B
+    assert t.pick_variant("jenkins", n, (32 * n, 32, 32)) == RS
     assert t.pick_variant("md5", n, (32 * n, 32, 32)) == DIRECT | PADTAB
     # short fixed, long keys (C4)
     assert t.pick_variant("fnv1a_64", n, (8 * n, 8, 8)) == WG

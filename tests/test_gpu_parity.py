@@ -380,6 +380,43 @@ def test_wave_ring_crc_sliced(gpu, oracle, var):
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
 
 
+@pytest.mark.parametrize("depth_bits,slice_bits", [(0, 0), (1, 1), (2, 2), (0, 3)],
+                         ids=["ahead2-s4", "ahead1-s8", "ahead3-s16", "ahead2-s16r4"])
+def test_direct_short_keys(gpu, oracle, depth_bits, slice_bits):
+    """The byte modes' short-key kernel (variant bit 11 with the direct
+    pipeline: keys of at most 16 or 32 bytes by the caller's shape, eight
+    waves per CU on a persistent grid, 1-3 tiles in flight per wave) on
+    ragged batch sizes (fewer tiles than waves, a partial last tile) and
+    misaligned buffers, and with a shape that understates the longest key
+    (from that tile on, the slow loop from global memory), against the
+    oracle. The crcs by slicing-by-4, -8 and -16 tables (variant bits 22-23)."""
+    var = (1 << 19) | (1 << 11) | (depth_bits << 20) | (slice_bits << 22)
+    L.lib().nc_gpuhash_set_tuning(0, 0, var)
+    import torch
+
+    try:
+        cases = [(1, t.SynthSpec.fixed(80, 32), None), (65, t.SynthSpec.fixed(81, 32), None),
+                 (70001, t.SynthSpec.fixed(82, 32), None), (4097, t.SynthSpec.fixed(83, 16), None),
+                 (3001, t.SynthSpec.fixed(84, 17), None), (5000, t.SynthSpec.uniform(85, 0, 32), None),
+                 (2049, t.SynthSpec.uniform(86, 0, 16), None), (1 << 20, t.SynthSpec.fixed(89, 32), None),
+                 (9000, t.SynthSpec.uniform(87, 0, 100), 32),  # the shape says <= 32: wrong for many tiles
+                 (300000, t.SynthSpec.uniform(90, 0, 40), 32),  # wrong in a few tiles of a long batch
+                 (3000, t.SynthSpec.uniform(88, 10, 40), 16)]  # says <= 16
+        for n, spec, claim in cases:
+            keys, off = t.synth_host(spec, 3, n)
+            lens = np.diff(off)
+            hi = int(lens.max()) if claim is None else claim
+            for shift in (0, 7):
+                kd, od = to_dev(keys, off, shift=shift)
+                for m in (0, 2, 3, 4, 5, 6, 7, 8):
+                    got = t.hash_batch_device(m, kd, od, shape=(int(off[-1]), int(lens.min()), hi))
+                    torch.cuda.synchronize()
+                    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), oracle.batch(m, keys, off),
+                                                  err_msg=f"var={var} n={n} spec={spec} claim={claim} mode={m}")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
 @pytest.mark.parametrize("var", [1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (8 << 20), (1 << 19) | (10 << 20),
                                  (1 << 19) | (11 << 20), (1 << 19) | (14 << 20), (1 << 19) | (9 << 20),
                                  (1 << 19) | (14 << 20) | (1 << 12), (1 << 19) | (10 << 20) | (1 << 13),

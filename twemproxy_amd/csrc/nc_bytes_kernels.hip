@@ -27,6 +27,8 @@ using namespace nc_direct;
 
 constexpr uint32_t kWaves = 16; /* 1024-thread workgroups share one table */
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
 template <int MODE>
 constexpr bool has_table()
 {
@@ -239,7 +241,261 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
 }
 
+/* the first nb (per lane, <= 16 * NC) key bytes of words d[0 .. NC); the crcs
+ * take NW words (slicing-by-4NW, tables in R copies) per dependent step where
+ * the whole group belongs to the key */
+template <int MODE, int NC, int NW, uint32_t R>
+__device__ __forceinline__ uint32_t short_step(uint32_t h, const u32x4 (&d)[NC], int32_t nb, const uint32_t *tab,
+                                               uint32_t lane4)
+{
+    constexpr int32_t kWhole = nc_slice::whole<MODE>();
+    if constexpr (has_table<MODE>() && NW > 1) {
+#pragma unroll
+        for (int t = 0; t < 4 * NC; t += NW) {
+            const int32_t kb = nb - 4 * t;
+            uint32_t w[NW];
+#pragma unroll
+            for (int i = 0; i < NW; i++) w[i] = d[(t + i) >> 2][(t + i) & 3];
+            if (kb >= kWhole + 4 * (NW - 1)) {
+                h = nc_slice::words<MODE, R, NW>(h, w, tab, lane4);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NW; i++) {
+                    if (kb - 4 * i >= kWhole) h = nc_slice::word<MODE, R>(h, w[i], tab, lane4);
+                    else if (kb - 4 * i > 0) h = nc_slice::bytes<MODE, R>(h, w[i], kb - 4 * i, tab, lane4);
+                }
+            }
+        }
+        return h;
+    }
+#pragma unroll
+    for (int t = 0; t < 4 * NC; t++) {
+        const int32_t kb = nb - 4 * t;
+        const uint32_t w = d[t >> 2][t & 3];
+        if (kb >= kWhole) h = word_step<MODE, R>(h, w, tab, lane4);
+        else if (kb > 0) h = bytes_step<MODE, R>(h, w, kb, tab, lane4);
+    }
+    return h;
+}
+
+/*
+ * Short keys (the caller's shape: every key at most 16 * NC bytes, C3's
+ * 32-byte keys): the direct pipeline's per-lane tiles at EIGHT waves per CU
+ * (one 512-thread workgroup, held alone on its CU by its LDS), a persistent
+ * grid of one workgroup per CU whose waves walk tiles interleaved over the
+ * whole batch, and DEPTH - 1 tiles of key bytes in flight per wave. The
+ * direct kernel's 32 waves per CU read and write HBM in too many concurrent
+ * streams: its memory pattern alone (no hash) runs 0.56-0.59 ms on C3, the
+ * same pattern at eight waves per CU with two tiles in flight 0.517
+ * (tools/probes/direct_depth.hip, profiles/r05_direct_depth.jsonl).
+ *
+ * Round j of a wave: issue the offsets of tile j + DEPTH, then tile
+ * j + DEPTH - 1's NC 16-byte loads per lane (its offsets came during round
+ * j - 1), then hash tile j (loaded DEPTH - 1 rounds ago) and store it. Every
+ * round issues the same loads (past the wave's last tile the last one is
+ * re-read), so hipcc's waitcnt pass counts them exactly and leaves the
+ * younger tiles in flight. A tile holding a longer key (the shape was wrong)
+ * ends the pipelined loop; that tile and the rest go block by block from
+ * global memory: slower, never wrong.
+ */
+template <int MODE, int NC, int DEPTH, int WAVES, int NW, uint32_t R>
+__global__ __launch_bounds__(64 * WAVES) void nc_bytes_short_kernel(const uint8_t *__restrict__ keys,
+                                                                   const uint64_t *__restrict__ off, uint64_t nkeys,
+                                                                   uint32_t *__restrict__ out, uint64_t ntiles)
+{
+    static_assert(NC >= 1 && NC <= 2 && DEPTH >= 2 && DEPTH <= 4, "short keys, 1-3 tiles ahead");
+    constexpr uint32_t kTabWords = nc_slice::table_words<R, 4u * NW>();
+    __shared__ uint32_t tab[has_table<MODE>() ? kTabWords : 1];
+    if constexpr (has_table<MODE>()) {
+        nc_slice::fill<MODE, R, 4u * NW>(tab, threadIdx.x, 64u * WAVES);
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane4 = nc_slice::copy_of<R>(lane);
+    const Tiles<true> tiles = wave_tiles<true>(ntiles, 0xffffffffu, WAVES, wave);
+    const uint32_t n = tiles.n;
+    if (n == 0u) return;
+    const uint32_t nk32 = (uint32_t)nkeys;
+    const uint64_t kbytes = off[nkeys] + (uint64_t)NC_GPUHASH_PAD;
+
+    /* The crcs take a tile's base (off[k0]) from lane 0's vector-loaded
+     * start (v_readfirstlane once the loads are waited for): a scalar load of
+     * it shares lgkmcnt with the table's LDS reads, so every lookup's wait
+     * would also wait for the offsets of a tile DEPTH rounds ahead (measured:
+     * crc32 0.65 -> 0.60 ms on C3). The other modes read no LDS and keep the
+     * scalar load, whose own counter leaves the vector waits exact (their
+     * vector-base build measured 1-6 % slower). */
+    constexpr bool kVB = has_table<MODE>();
+    struct Offs {
+        uint32_t s, s_hi, e;
+        uint64_t s0;
+    };
+    auto key0 = [&](uint32_t j) { return tiles.at(j < n ? j : n - 1u) * 64u; };
+    auto load_off = [&](uint32_t j) __attribute__((always_inline)) {
+        const uint32_t k0 = key0(j);
+        const rsrc_t r = make_rsrc(off + k0, ((uint64_t)(nk32 - k0) + 1u) * 8u);
+        Offs o;
+        if constexpr (kVB) {
+            const u32x2 sv = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(lane * 8u), 0, kAuxNt);
+            o.s = sv.x;
+            o.s_hi = sv.y;
+            o.s0 = 0;
+        } else {
+            o.s = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u), 0, kAuxNt);
+            o.s_hi = 0;
+            o.s0 = off[k0];
+        }
+        o.e = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u + 8u), 0, kAuxNt);
+        return o;
+    };
+    auto base_of = [&](const Offs &o) __attribute__((always_inline)) {
+        if constexpr (!kVB) return o.s0;
+        return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)o.s) |
+               ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)o.s_hi) << 32);
+    };
+    auto load_data = [&](const Offs &o, u32x4 (&d)[NC]) __attribute__((always_inline)) {
+        const uint64_t s0 = base_of(o);
+        const rsrc_t r = make_rsrc(keys + s0, kbytes - s0);
+        const int vo = (int)(o.s - (uint32_t)s0);
+#pragma unroll
+        for (int c = 0; c < NC; c++) d[c] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16 * c, 0, 0);
+    };
+
+    u32x4 dat[DEPTH][NC];
+    uint32_t klen[DEPTH]; /* the tiles' key lengths */
+    Offs ob[DEPTH];       /* offsets ring: tile j's in ob[j % DEPTH] (period DEPTH, as the unrolled rounds) */
+    /* prologue: tiles 0 .. DEPTH - 2 in flight, offsets of tile DEPTH - 1 */
+#pragma unroll
+    for (int q = 0; q < DEPTH - 1; q++) {
+        const Offs o = load_off((uint32_t)q);
+        klen[q] = o.e - o.s;
+        load_data(o, dat[q]);
+    }
+    ob[DEPTH - 1] = load_off((uint32_t)(DEPTH - 1));
+
+    uint32_t jbad = n; /* the first tile with a key longer than 16 * NC bytes */
+    for (uint32_t j0 = 0; jbad == n && j0 < n; j0 += DEPTH) {
+#pragma unroll
+        for (int q = 0; q < DEPTH; q++) {
+            const uint32_t j = j0 + (uint32_t)q;
+            if (j >= n) break;
+            const int qa = (q + DEPTH - 1) % DEPTH; /* the data set tile j + DEPTH - 1 goes to */
+            ob[q] = load_off(j + (uint32_t)DEPTH);  /* (j + DEPTH) % DEPTH == q */
+            klen[qa] = ob[qa].e - ob[qa].s;
+            load_data(ob[qa], dat[qa]);
+            const uint32_t k0 = tiles.at(j) * 64u;
+            const uint32_t nv = nk32 - k0 < 64u ? nk32 - k0 : 64u;
+            const uint32_t len = klen[q];
+            if (__ballot(lane < nv && len > 16u * NC) != 0ull) { /* the shape was wrong: the slow loop below */
+                jbad = j;
+                break;
+            }
+            const uint32_t h = short_step<MODE, NC, NW, R>(init_state<MODE>(), dat[q], (int32_t)len, tab, lane4);
+            const rsrc_t rout = make_rsrc(out + k0, 4u * nv); /* lanes past the batch: dropped */
+            __builtin_amdgcn_raw_buffer_store_b32(final_state<MODE>(h), rout, (int)(lane * 4u), 0, kAuxNt);
+        }
+    }
+    /* tiles jbad .. n - 1 (only when a key was longer than the shape said),
+     * outside the pipelined loop so that its waits stay exact: 64-byte blocks
+     * from global memory, one tile at a time */
+    for (uint32_t j = jbad; j < n; j++) {
+        const Offs o = load_off(j);
+        const uint32_t k0 = tiles.at(j) * 64u;
+        const uint32_t nv = nk32 - k0 < 64u ? nk32 - k0 : 64u;
+        const uint64_t s0 = base_of(o);
+        const rsrc_t r = make_rsrc(keys + s0, kbytes - s0);
+        const uint32_t vo = o.s - (uint32_t)s0;
+        int32_t rem = lane < nv ? (int32_t)(o.e - o.s) : 0;
+        uint32_t h = init_state<MODE>();
+        for (uint32_t b = 0; __ballot(rem > 0) != 0ull; b++) {
+            u32x4 d4[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                d4[c] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(vo + 64u * b + 16u * (uint32_t)c), 0, 0);
+            if (rem > 0) {
+#pragma unroll
+                for (int t = 0; t < 16; t++) {
+                    const int32_t kb = rem - 4 * t;
+                    const uint32_t w = d4[t >> 2][t & 3];
+                    if (kb >= nc_slice::whole<MODE>()) h = word_step<MODE, R>(h, w, tab, lane4);
+                    else if (kb > 0) h = bytes_step<MODE, R>(h, w, kb, tab, lane4);
+                }
+            }
+            rem -= 64;
+        }
+        const rsrc_t rout = make_rsrc(out + k0, 4u * nv);
+        __builtin_amdgcn_raw_buffer_store_b32(final_state<MODE>(h), rout, (int)(lane * 4u), 0, kAuxNt);
+    }
+}
+
 namespace nc_bytes {
+
+static int num_cus()
+{
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            n = v;
+        else
+            return 256;
+    }
+    return n;
+}
+
+/* the short-key kernel: every key <= 16 * NC bytes; a persistent grid of
+ * one eight-wave workgroup per CU (dynamic LDS keeps a second one out);
+ * var bits 0-1 the depth (3, 2, 4 tiles: 2, 1, 3 ahead), bits 2-3 the crcs'
+ * tables (slicing-by-4 in 8 copies, by-8 in 8 copies, by-16 in 8, by-16 in 4) */
+template <int MODE, int NC, int DEPTH, int NW, uint32_t R>
+hipError_t launch_short_t(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
+                          hipStream_t stream)
+{
+    constexpr int kW = 8;
+    const uint64_t ntiles = (nkeys + 63u) / 64u;
+    uint64_t grid = (uint64_t)num_cus();
+    const uint64_t need = (ntiles + kW - 1u) / kW;
+    if (grid > need) grid = need;
+    /* more than half the CU's 160 KiB in all: one workgroup per CU */
+    constexpr uint32_t kTab = has_table<MODE>() ? nc_slice::table_words<R, 4u * NW>() * 4u : 0u;
+    const uint32_t pad = kTab >= 90112u ? 0u : 90112u - kTab;
+    auto k = nc_bytes_short_kernel<MODE, NC, DEPTH, kW, NW, R>;
+    static const bool attr = [&] { /* once per instantiation (and process: one device kind) */
+        (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad);
+        return true;
+    }();
+    (void)attr;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * kW), pad, stream, d_keys, d_off, nkeys, d_out, ntiles);
+    return hipGetLastError();
+}
+
+template <int MODE, int NC, int DEPTH>
+hipError_t launch_short_d(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
+                          hipStream_t stream, int var)
+{
+    if constexpr (has_table<MODE>()) {
+        switch ((var >> 2) & 3) {
+        case 1: return launch_short_t<MODE, NC, DEPTH, 2, 8>(d_keys, d_off, nkeys, d_out, stream);
+        case 2: return launch_short_t<MODE, NC, DEPTH, 4, 8>(d_keys, d_off, nkeys, d_out, stream);
+        case 3: return launch_short_t<MODE, NC, DEPTH, 4, 4>(d_keys, d_off, nkeys, d_out, stream);
+        default: break;
+        }
+    }
+    return launch_short_t<MODE, NC, DEPTH, 1, 8>(d_keys, d_off, nkeys, d_out, stream);
+}
+
+template <int MODE, int NC>
+hipError_t launch_short(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
+                        hipStream_t stream, int var)
+{
+    switch (var & 3) {
+    case 1: return launch_short_d<MODE, NC, 2>(d_keys, d_off, nkeys, d_out, stream, var);
+    case 2: return launch_short_d<MODE, NC, 4>(d_keys, d_off, nkeys, d_out, stream, var);
+    default: return launch_short_d<MODE, NC, 3>(d_keys, d_off, nkeys, d_out, stream, var);
+    }
+}
 
 template <int MODE, int OPT>
 hipError_t launch_opt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
@@ -283,11 +539,16 @@ hipError_t launch_opt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nke
 }
 
 /* var bits 5-6: OPT (bit 5 slicing-by-8 crcs, bit 6 the DIAGNOSTIC no-hash
- * build, fnv1a_64 and crc32 only) */
+ * build, fnv1a_64 and crc32 only); bit 7: the short-key kernel for keys of at
+ * most max_len (<= 32) bytes */
 template <int MODE>
 hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
-                       hipStream_t stream, int var)
+                       hipStream_t stream, int var, uint32_t max_len)
 {
+    if ((var & 128) && max_len <= 32u) {
+        if (max_len <= 16u) return launch_short<MODE, 1>(d_keys, d_off, nkeys, d_out, stream, var);
+        return launch_short<MODE, 2>(d_keys, d_off, nkeys, d_out, stream, var);
+    }
     if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_CRC32) {
         if (var & 64) return launch_opt<MODE, kOptNoHash>(d_keys, d_off, nkeys, d_out, stream, var);
     }
@@ -300,7 +561,8 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
 /* the byte-serial modes on the direct pipeline; var: bits 0-1 tiles per wave
  * (16, 8, 32, 64), bit 2 the LDS-DMA block image (long keys), bit 3 a wave's
  * tiles interleaved over the grid (else consecutive), bit 4 (with 2 and 3)
- * eight-wave workgroups, one per CU. nkeys < 2^32. */
+ * eight-wave workgroups, one per CU, bits 5-7 as launch_mode. max_len: the
+ * caller's longest key (its shape; 0xffffffff unknown). nkeys < 2^32. */
 bool supports(int mode)
 {
     switch (mode) {
@@ -319,17 +581,17 @@ bool supports(int mode)
 }
 
 hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
-                  hipStream_t stream, int var)
+                  hipStream_t stream, int var, uint32_t max_len)
 {
     switch (mode) {
-    case NC_GPUHASH_ONE_AT_A_TIME: return launch_mode<NC_GPUHASH_ONE_AT_A_TIME>(d_keys, d_off, nkeys, d_out, stream, var);
-    case NC_GPUHASH_CRC16: return launch_mode<NC_GPUHASH_CRC16>(d_keys, d_off, nkeys, d_out, stream, var);
-    case NC_GPUHASH_CRC32: return launch_mode<NC_GPUHASH_CRC32>(d_keys, d_off, nkeys, d_out, stream, var);
-    case NC_GPUHASH_CRC32A: return launch_mode<NC_GPUHASH_CRC32A>(d_keys, d_off, nkeys, d_out, stream, var);
-    case NC_GPUHASH_FNV1_64: return launch_mode<NC_GPUHASH_FNV1_64>(d_keys, d_off, nkeys, d_out, stream, var);
-    case NC_GPUHASH_FNV1A_64: return launch_mode<NC_GPUHASH_FNV1A_64>(d_keys, d_off, nkeys, d_out, stream, var);
-    case NC_GPUHASH_FNV1_32: return launch_mode<NC_GPUHASH_FNV1_32>(d_keys, d_off, nkeys, d_out, stream, var);
-    case NC_GPUHASH_FNV1A_32: return launch_mode<NC_GPUHASH_FNV1A_32>(d_keys, d_off, nkeys, d_out, stream, var);
+    case NC_GPUHASH_ONE_AT_A_TIME: return launch_mode<NC_GPUHASH_ONE_AT_A_TIME>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
+    case NC_GPUHASH_CRC16: return launch_mode<NC_GPUHASH_CRC16>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
+    case NC_GPUHASH_CRC32: return launch_mode<NC_GPUHASH_CRC32>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
+    case NC_GPUHASH_CRC32A: return launch_mode<NC_GPUHASH_CRC32A>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
+    case NC_GPUHASH_FNV1_64: return launch_mode<NC_GPUHASH_FNV1_64>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
+    case NC_GPUHASH_FNV1A_64: return launch_mode<NC_GPUHASH_FNV1A_64>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
+    case NC_GPUHASH_FNV1_32: return launch_mode<NC_GPUHASH_FNV1_32>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
+    case NC_GPUHASH_FNV1A_32: return launch_mode<NC_GPUHASH_FNV1A_32>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
     default: return hipErrorInvalidValue;
     }
 }

@@ -132,6 +132,31 @@ __device__ __forceinline__ uint32_t word2(uint32_t h, uint32_t w0, uint32_t w1, 
     }
 }
 
+/* the 4 * NW bytes of words w[0 .. NW) (slicing-by-4NW: NW = 1, 2, 4 words,
+ * one dependent step); byte i of the group through table 4 * NW - 1 - i */
+template <int MODE, uint32_t R, int NW>
+__device__ __forceinline__ uint32_t words(uint32_t h, const uint32_t *w, const uint32_t *tab, uint32_t cb)
+{
+    constexpr uint32_t T = 4u * NW - 1u;
+    uint32_t acc = 0u;
+    if constexpr (MODE == NC_GPUHASH_CRC16) {
+#pragma unroll
+        for (int i = 0; i < NW; i++) {
+            const uint32_t v = (i == 0 ? (h & 0xffffu) << 16 : 0u) ^ __builtin_bswap32(w[i]);
+            acc ^= (look<R>(tab, v >> 24, cb, T - 4u * i) ^ look<R>(tab, (v >> 16) & 0xffu, cb, T - 4u * i - 1u)) ^
+                   (look<R>(tab, (v >> 8) & 0xffu, cb, T - 4u * i - 2u) ^ look<R>(tab, v & 0xffu, cb, T - 4u * i - 3u));
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < NW; i++) {
+            const uint32_t x = (i == 0 ? h : 0u) ^ w[i];
+            acc ^= (look<R>(tab, x & 0xffu, cb, T - 4u * i) ^ look<R>(tab, (x >> 8) & 0xffu, cb, T - 4u * i - 1u)) ^
+                   (look<R>(tab, (x >> 16) & 0xffu, cb, T - 4u * i - 2u) ^ look<R>(tab, x >> 24, cb, T - 4u * i - 3u));
+        }
+    }
+    return acc;
+}
+
 /* a word is taken whole only when at least kWhole key bytes start at it */
 template <int MODE>
 constexpr int32_t whole()

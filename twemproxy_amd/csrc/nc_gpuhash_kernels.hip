@@ -1890,7 +1890,7 @@ namespace nc_bytes {
 /* the byte-serial modes on the direct pipeline (nc_bytes_kernels.hip) */
 bool supports(int mode);
 hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
-                  hipStream_t stream, int var);
+                  hipStream_t stream, int var, uint32_t max_len);
 } // namespace nc_bytes
 
 namespace nc_wsort {
@@ -1938,7 +1938,8 @@ constexpr int kVarDirect8 = 1 << 12;     /* line image: eight-wave workgroups, o
 constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
 constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
 constexpr int kVarMd5PadTab = 1 << 15;    /* md5: padding selectors from an LDS table */
-static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash | kVarMd5PadTab) &
+constexpr int kVarDirectShort = 1 << 11;  /* byte modes, keys <= 32 B: eight waves per CU, tiles in flight */
+static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash | kVarMd5PadTab | kVarDirectShort) &
                (kVarMd5Direct | (15 << 20) | kVarNoFixedLen | kVarWsort | kVarGsort | kVarNoPacked | (3 << 29))) == 0,
               "direct-pipeline options overlap the pipeline choice, its nibble or the server_idx bits");
 
@@ -2435,6 +2436,15 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
         if (mode == NC_GPUHASH_HSIEH) return kVarRingP5;
         return kVarRingP4;
     }
+    /* fixed-length keys of 20-32 bytes (C3): the direct pipeline's short-key
+     * kernel (eight waves per CU, persistent, three tiles in flight per wave)
+     * for crc32 / crc32a (slicing-by-8 tables) and one_at_a_time: C3 crc32
+     * 0.578 -> 0.541 ms, crc32a 0.580 -> 0.541, one_at_a_time 0.581 -> 0.525
+     * (profiles/r05_c3_short8_ab2.jsonl); crc16 0.580 -> 0.603 keeps the
+     * 32-wave kernel, the fnvs tie the wave ring (0.522-0.529) and keep it */
+    if (fixed && mean >= 20u && sh->max_len <= 32u &&
+        (mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A || mode == NC_GPUHASH_ONE_AT_A_TIME))
+        return kVarDirect | kVarDirectShort | (2 << 20) | (mode == NC_GPUHASH_ONE_AT_A_TIME ? 0 : (1 << 22));
     /* fixed-length short keys: the crcs' slicing-by-4 tables on the direct
      * pipeline (C3: 0.70 -> 0.61 ms); varying lengths keep the length-grouped
      * workgroup pipelines (a direct wave runs to its longest key) */
@@ -2503,7 +2513,9 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
         if (nc_bytes::supports(mode))
             return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream,
                                     ((var >> 20) & 15) | ((var & kVarDirect8) != 0 ? 16 : 0) |
-                                        ((var & kVarDirectS8) != 0 ? 32 : 0) | ((var & kVarDirectNoHash) != 0 ? 64 : 0));
+                                        ((var & kVarDirectS8) != 0 ? 32 : 0) | ((var & kVarDirectNoHash) != 0 ? 64 : 0) |
+                                        ((var & kVarDirectShort) != 0 ? 128 : 0),
+                                    shape != nullptr && nkeys != 0 ? (uint32_t)shape->max_len : 0xffffffffu);
     }
     if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))
         return nc_wsort::launch(mode, d_keys, d_off, nkeys, d_out, stream, (var >> 20) & 15);
