@@ -381,7 +381,7 @@ def test_wave_ring_crc_sliced(gpu, oracle, var):
 
 
 @pytest.mark.parametrize("depth_bits,slice_bits", [(0, 0), (1, 1), (2, 2), (0, 3)],
-                         ids=["ahead2-s4", "ahead1-s8", "ahead3-s16", "ahead2-s16r4"])
+                         ids=["ahead2-s4", "ahead1-s8", "ahead3-s16", "ahead2-s4r32"])
 def test_direct_short_keys(gpu, oracle, depth_bits, slice_bits):
     """The byte modes' short-key kernel (variant bit 11 with the direct
     pipeline: keys of at most 16 or 32 bytes by the caller's shape, eight
@@ -389,7 +389,8 @@ def test_direct_short_keys(gpu, oracle, depth_bits, slice_bits):
     ragged batch sizes (fewer tiles than waves, a partial last tile) and
     misaligned buffers, and with a shape that understates the longest key
     (from that tile on, the slow loop from global memory), against the
-    oracle. The crcs by slicing-by-4, -8 and -16 tables (variant bits 22-23)."""
+    oracle. The crcs by slicing-by-4, -8 and -16 tables (variant bits 22-23;
+    by-4 also in 32 copies)."""
     var = (1 << 19) | (1 << 11) | (depth_bits << 20) | (slice_bits << 22)
     L.lib().nc_gpuhash_set_tuning(0, 0, var)
     import torch

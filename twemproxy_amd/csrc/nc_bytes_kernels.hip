@@ -303,7 +303,7 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_short_kernel(const uint8_
                                                                    const uint64_t *__restrict__ off, uint64_t nkeys,
                                                                    uint32_t *__restrict__ out, uint64_t ntiles)
 {
-    static_assert(NC >= 1 && NC <= 2 && DEPTH >= 2 && DEPTH <= 4, "short keys, 1-3 tiles ahead");
+    static_assert(NC >= 1 && NC <= 2 && DEPTH >= 2 && DEPTH <= 4, "keys of <= 16 or 32 B; 1-3 tiles ahead");
     constexpr uint32_t kTabWords = nc_slice::table_words<R, 4u * NW>();
     __shared__ uint32_t tab[has_table<MODE>() ? kTabWords : 1];
     if constexpr (has_table<MODE>()) {
@@ -447,7 +447,8 @@ static int num_cus()
 /* the short-key kernel: every key <= 16 * NC bytes; a persistent grid of
  * one eight-wave workgroup per CU (dynamic LDS keeps a second one out);
  * var bits 0-1 the depth (3, 2, 4 tiles: 2, 1, 3 ahead), bits 2-3 the crcs'
- * tables (slicing-by-4 in 8 copies, by-8 in 8 copies, by-16 in 8, by-16 in 4) */
+ * tables (slicing-by-4 in 8 copies, by-8 in 8 copies, by-16 in 8, by-4 in 32:
+ * one copy per lane of a ds_read_b32 lane group, conflict-free) */
 template <int MODE, int NC, int DEPTH, int NW, uint32_t R>
 hipError_t launch_short_t(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
                           hipStream_t stream)
@@ -479,7 +480,7 @@ hipError_t launch_short_d(const uint8_t *d_keys, const uint64_t *d_off, uint64_t
         switch ((var >> 2) & 3) {
         case 1: return launch_short_t<MODE, NC, DEPTH, 2, 8>(d_keys, d_off, nkeys, d_out, stream);
         case 2: return launch_short_t<MODE, NC, DEPTH, 4, 8>(d_keys, d_off, nkeys, d_out, stream);
-        case 3: return launch_short_t<MODE, NC, DEPTH, 4, 4>(d_keys, d_off, nkeys, d_out, stream);
+        case 3: return launch_short_t<MODE, NC, DEPTH, 1, 32>(d_keys, d_off, nkeys, d_out, stream);
         default: break;
         }
     }
