@@ -32,7 +32,7 @@ BENCH_PHASES = [("C2 fnv1a_64", 20), ("C2 md5", 10), ("C2 server_idx ketama", 10
 PMC_LEGS = [("C2", "C2", "fnv1a_64"), ("C2", "C2", "md5"), ("C2", "C2", "server_idx"), ("C3", "C3", "fnv1a_64"),
             ("C3", "C3", "crc32"), ("C3", "C3", "md5"), ("C4S", "C4", "md5"), ("C4S", "C4", "crc32"),
             ("C4S", "C4", "fnv1a_64")]
-HASH_KERNELS = ("nc_hash_kernel", "nc_md5_", "nc_bytes_direct")
+HASH_KERNELS = ("nc_hash_kernel", "nc_md5_", "nc_bytes_direct", "nc_bytes_short")
 
 
 def is_hash_kernel(name):
@@ -82,7 +82,7 @@ def modes(src, rnd):
         """hash mode of a kernel name: the first template argument, or md5 for its own kernels"""
         if "nc_md5_" in name:
             return "md5"
-        mm = re.search(r"(?:nc_hash_kernel(?:_rs|_wr)?|nc_bytes_direct_kernel)<(?:mode=)?(\d+)", name)
+        mm = re.search(r"(?:nc_hash_kernel(?:_rs|_wr)?|nc_bytes_direct_kernel|nc_bytes_short_kernel)<(?:mode=)?(\d+)", name)
         return MODE_NAMES[int(mm.group(1))] if mm else None
 
     stats = os.path.join(src, "trace", "modes_kernel_stats.csv")
