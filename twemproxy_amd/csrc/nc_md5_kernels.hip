@@ -36,6 +36,8 @@
 
 #include <stdint.h>
 
+#include <array>
+#include <type_traits>
 #include <utility>
 
 #include "nc_gpuhash.h"
@@ -59,6 +61,14 @@ struct Queue {
     uint32_t *w; /* SoA: w[f * kQ + slot] */
     uint32_t head, count; /* wave-uniform */
 };
+
+/* the lanes where p holds, as a wave mask: the builtin straight from the
+ * compare's mask (HIP's __ballot(int) widens the bool to a VGPR 0/1 and
+ * compares it again: two VALU per use) */
+__device__ __forceinline__ uint64_t ballot(bool p)
+{
+    return __builtin_amdgcn_ballot_w64(p);
+}
 
 __device__ __forceinline__ uint32_t lanemask_lt_popc(uint64_t m)
 {
@@ -191,6 +201,8 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
     u32x4 da[4], db[4];
     load_blk(cur_t, 0u, da);
     uint32_t b = 0;
+    /* the chaining state of keys with a later block (set by block 0's round;
+     * a first block starts from the constants, md5_steps_first61) */
     uint32_t st[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
     uint32_t pad_src; /* kPadSrc in a VGPR: a uniform selector takes the perm's SGPR slot */
     asm volatile("v_mov_b32 %0, %1" : "=v"(pad_src) : "i"(kPadSrc));
@@ -206,18 +218,24 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
      * out before the next round's loads could land there (24 v_mov per round
      * in the fixed-length form). */
     auto round = [&](u32x4 (&cur)[4], u32x4 (&nxt)[4]) __attribute__((always_inline)) {
-        const bool more = __ballot((lane < cur_t.nv) && cur_t.len > 64u * (b + 1u)) != 0ull;
+        const bool more = ballot((lane < cur_t.nv) && cur_t.len > 64u * (b + 1u)) != 0ull;
         const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
         const int32_t rem = (int32_t)cur_t.len - 64 * (int32_t)b; /* key bytes from this block's start */
         const uint32_t len = cur_t.len;
         const bool act = (lane < cur_t.nv) && rem > 0;
+        /* keys whose last data block could not take the length (or empty
+         * keys) queue their state for a data-free tail block; the mask is
+         * taken here, under the full exec mask (inside the steps' divergent
+         * region hipcc rebuilds it with a select and a compare) */
+        const bool tail = (lane < cur_t.nv) && ((rem <= 64 && rem >= 56) || (b == 0u && len == 0u));
+        const uint64_t tm = ballot(tail);
         if constexpr (LDS) wk.read_img(img, cur); /* this round's block, DMA'd during the previous round */
         /* FL: a tile whose keys all have FL bytes (checked: the shape only
          * picks the instantiation) takes its data words as loaded, the
          * boundary word by one constant perm, and constants for the rest.
          * Every form pads `cur` in place: the steps read it as it stands. */
         bool fl_tile = false;
-        if constexpr (FL > 0) fl_tile = __ballot((lane < cur_t.nv) && cur_t.len != (uint32_t)FL) == 0ull;
+        if constexpr (FL > 0) fl_tile = ballot((lane < cur_t.nv) && cur_t.len != (uint32_t)FL) == 0ull;
         if (fl_tile) {
             if constexpr (FL > 0 && FL % 4 != 0) {
                 constexpr uint32_t bnd = FL % 4 == 1 ? kBoundary1 : (FL % 4 == 2 ? kBoundary2 : kBoundary3);
@@ -245,42 +263,61 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
         no = wk.template load_off<0>(more ? tile + 1u : tile + 2u);
         if (fl_tile) {
             if constexpr (FL > 0) {
-                if (act) {
-                    uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+                if (act) { /* one block: from the initial state */
+                    uint32_t v[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
                     md5_steps_fl<FL>(v, w, std::make_integer_sequence<int, 61>{});
                     const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
-                    __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
+                    __builtin_amdgcn_raw_buffer_store_b32(NC_MD5_A0 + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
                 }
             }
         }
-        if (!fl_tile) { /* (a fixed-length tile, FL <= 48, has no tail keys) */
-            uint32_t v[4] = {st[0], st[1], st[2], st[3]}; /* a queued key's X (run_tail) */
+        /* a tile's block 0 (wave-uniform b) starts from the constant state:
+         * its own copy of the steps folds it in, and nothing resets st */
+        auto gen = [&](auto first_c) __attribute__((always_inline)) {
+            constexpr bool FIRST = decltype(first_c)::value;
+            uint32_t v[4]; /* a queued key's X (run_tail) */
+            if constexpr (FIRST) {
+                v[0] = NC_MD5_A0;
+                v[1] = NC_MD5_B0;
+                v[2] = NC_MD5_C0;
+                v[3] = NC_MD5_D0;
+            } else {
+                v[0] = st[0];
+                v[1] = st[1];
+                v[2] = st[2];
+                v[3] = st[3];
+            }
             if (act) {
                 const bool fin = rem <= 55;
                 /* steps 0..60 for every lane; a key that ends here is done (A's
                  * last update is step 60); a key of 56..64 bytes leaves steps
                  * 61..63 to its tail block's round (run_tail); longer keys run
                  * them here */
-                md5_steps(v, w, std::make_integer_sequence<int, 61>{});
+                if constexpr (FIRST) md5_steps_first61(v, w);
+                else md5_steps(v, w, std::make_integer_sequence<int, 61>{});
                 if (fin) {
                     const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
-                    __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
+                    __builtin_amdgcn_raw_buffer_store_b32((FIRST ? NC_MD5_A0 : st[0]) + v[0], rout, (int)(lane * 4u),
+                                                          0, kAuxNt);
                 } else if (len - 56u > 8u) {
                     md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
-                    st[0] += v[0];
-                    st[1] += v[1];
-                    st[2] += v[2];
-                    st[3] += v[3];
+                    st[0] = (FIRST ? NC_MD5_A0 : st[0]) + v[0];
+                    st[1] = (FIRST ? NC_MD5_B0 : st[1]) + v[1];
+                    st[2] = (FIRST ? NC_MD5_C0 : st[2]) + v[2];
+                    st[3] = (FIRST ? NC_MD5_D0 : st[3]) + v[3];
                     v[0] = st[0];
                     v[1] = st[1];
                     v[2] = st[2];
                     v[3] = st[3];
                 }
             }
+            return std::array<uint32_t, 4>{v[0], v[1], v[2], v[3]};
+        };
+        if (!fl_tile) { /* (a fixed-length tile, FL <= 48, has no tail keys) */
+            const std::array<uint32_t, 4> v = b == 0u ? gen(std::true_type{}) : gen(std::false_type{});
             /* keys whose last data block could not take the length (or empty
              * keys) queue their state for a data-free tail block */
-            const bool tail = (lane < cur_t.nv) && ((rem <= 64 && rem >= 56) || (b == 0u && len == 0u));
-            const uint64_t tm = __ballot(tail);
+
             if (tm != 0ull) {
                 if (tail) {
                     const uint32_t slot = (q.head + q.count + lanemask_lt_popc(tm)) & (kQ - 1u);
@@ -306,10 +343,6 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
             tile++;
             b = 0;
             cur_t = nxt_t;
-            st[0] = NC_MD5_A0;
-            st[1] = NC_MD5_B0;
-            st[2] = NC_MD5_C0;
-            st[3] = NC_MD5_D0;
         }
     };
     for (;;) {

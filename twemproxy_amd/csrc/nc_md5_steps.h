@@ -59,6 +59,38 @@ __device__ __forceinline__ void md5_steps(uint32_t (&v)[4], const uint32_t (&w)[
     (md5_step<I>(v, w), ...);
 }
 
+/* steps OFF, OFF + 1, ... */
+template <int OFF, int... I>
+__device__ __forceinline__ void md5_steps_at(uint32_t (&v)[4], const uint32_t (&w)[16], std::integer_sequence<int, I...>)
+{
+    (md5_step<OFF + I>(v, w), ...);
+}
+
+/* Steps 0..3 of a key's FIRST block, whose state word v[u] is still the
+ * initial constant (RFC 1321 A0..D0): v[u] + T folds into one constant (an
+ * SGPR operand of v_add3), and step 0's round function is a constant too —
+ * four VALU per step, three for step 0. Past step 3 every state word is data. */
+template <int I>
+__device__ __forceinline__ void md5_step_first(uint32_t (&v)[4], const uint32_t (&w)[16])
+{
+    static_assert(I < 4, "the initial state is constant only through step 3");
+    constexpr uint32_t kInit[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
+    constexpr int u = (4 - (I & 3)) & 3;
+    const uint32_t b = v[(u + 1) & 3], c = v[(u + 2) & 3], d = v[(u + 3) & 3];
+    const uint32_t f = md5_f<I>(b, c, d);
+    v[u] = nc_rotl(w[kM[I]] + f + (kInit[u] + kT[I]), kS[I]) + b;
+}
+
+/* steps 0..60 of a key's first block from the initial state (v holds it) */
+__device__ __forceinline__ void md5_steps_first61(uint32_t (&v)[4], const uint32_t (&w)[16])
+{
+    md5_step_first<0>(v, w);
+    md5_step_first<1>(v, w);
+    md5_step_first<2>(v, w);
+    md5_step_first<3>(v, w);
+    md5_steps_at<4>(v, w, std::make_integer_sequence<int, 57>{});
+}
+
 template <int... I>
 __device__ __forceinline__ void md5_steps_from61(uint32_t (&v)[4], const uint32_t (&w)[16],
                                                  std::integer_sequence<int, I...>)
