@@ -383,13 +383,14 @@ def test_wave_ring_crc_sliced(gpu, oracle, var):
 @pytest.mark.parametrize("depth_bits,slice_bits", [(0, 0), (1, 1), (2, 2), (0, 3)],
                          ids=["ahead2-s4", "ahead1-s8", "ahead3-s16", "ahead2-s4r32"])
 def test_direct_short_keys(gpu, oracle, depth_bits, slice_bits):
-    """The byte modes' short-key kernel (variant bit 11 with the direct
+    """The short-key kernel (variant bit 11 with the direct
     pipeline: keys of at most 16 or 32 bytes by the caller's shape, eight
     waves per CU on a persistent grid, 1-3 tiles in flight per wave) on
     ragged batch sizes (fewer tiles than waves, a partial last tile) and
     misaligned buffers, and with a shape that understates the longest key
     (from that tile on, the slow loop from global memory), against the
-    oracle. The crcs by slicing-by-4, -8 and -16 tables (variant bits 22-23;
+    oracle, for the byte modes and the word modes (hsieh, murmur, jenkins).
+    The crcs by slicing-by-4, -8 and -16 tables (variant bits 22-23;
     by-4 also in 32 copies)."""
     var = (1 << 19) | (1 << 11) | (depth_bits << 20) | (slice_bits << 22)
     L.lib().nc_gpuhash_set_tuning(0, 0, var)
@@ -409,7 +410,7 @@ def test_direct_short_keys(gpu, oracle, depth_bits, slice_bits):
             hi = int(lens.max()) if claim is None else claim
             for shift in (0, 7):
                 kd, od = to_dev(keys, off, shift=shift)
-                for m in (0, 2, 3, 4, 5, 6, 7, 8):
+                for m in (0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11):
                     got = t.hash_batch_device(m, kd, od, shape=(int(off[-1]), int(lens.min()), hi))
                     torch.cuda.synchronize()
                     np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), oracle.batch(m, keys, off),

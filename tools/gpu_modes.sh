@@ -14,7 +14,7 @@ step() {
     timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
     local rc=$?; echo "   rc=$rc"; [ $rc -eq 0 ] || tail -n 20 "$OUT/$name.log"; return $rc
 }
-step sweep 500 python3 tools/sweep.py --configs C3 --modes $MODES --variants 0:0:0,0:0:65536,0:0:32,0:0:896,0:1:65536,0:0:524288 --rounds 3 || exit $?
+step sweep 500 python3 tools/sweep.py --configs C3 --modes $MODES --variants 0:0:0,0:0:65536,0:0:32,0:0:896,0:1:65536,0:0:524288,0:0:526336 --rounds 3 || exit $?
 step trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o modes --output-format csv -- \
     python3 tools/pmc_run.py --config C3 --mode $MODES --variant 0:0:0 --iters 10 || exit $?
 for ctr in FETCH_SIZE WRITE_SIZE; do

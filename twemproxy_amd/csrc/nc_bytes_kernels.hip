@@ -20,6 +20,7 @@
 #include "nc_direct.h"
 #include "nc_gpuhash.h"
 #include "nc_hash_algo.h"
+#include "nc_hash_key.h"
 
 namespace {
 
@@ -33,6 +34,14 @@ template <int MODE>
 constexpr bool has_table()
 {
     return MODE == NC_GPUHASH_CRC16 || MODE == NC_GPUHASH_CRC32 || MODE == NC_GPUHASH_CRC32A;
+}
+
+/* the word modes, on the short-key kernel only (src/hashkit/nc_hsieh.c,
+ * nc_murmur.c, nc_jenkins.c) */
+template <int MODE>
+constexpr bool is_word_mode()
+{
+    return MODE == NC_GPUHASH_HSIEH || MODE == NC_GPUHASH_MURMUR || MODE == NC_GPUHASH_JENKINS;
 }
 
 template <int MODE>
@@ -241,6 +250,61 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no LDS-DMA may outlive the workgroup */
 }
 
+/* A word mode's hash of a key of len (<= 16 * NC) bytes held from its first
+ * byte in d[0 .. NC) (the short-key kernel's unaligned loads put byte 0 of
+ * the key in byte 0 of d): hsieh SuperFastHash (src/hashkit/nc_hsieh.c:39-93),
+ * MurmurHash2 (nc_murmur.c:38-99), lookup3 hashlittle (nc_jenkins.c:76-230),
+ * as nc_lds_hash.h's stream forms but with every word index static (a
+ * lane's tail word by selects), so nothing leaves registers. */
+template <int MODE, int NC>
+__device__ __forceinline__ uint32_t short_words(const u32x4 (&d)[NC], uint32_t len)
+{
+    constexpr int NW = 4 * NC;
+    auto W = [&](int t) __attribute__((always_inline)) { return t < NW ? d[t >> 2][t & 3] : 0u; };
+    if constexpr (MODE == NC_GPUHASH_JENKINS) {
+        const uint32_t init = nc_jenkins_init(len);
+        uint32_t a = init, b = init, c = init;
+        constexpr int kMaxBlocks = (16 * NC - 1) / 12; /* 12-byte blocks before the last 1..12 bytes */
+        const uint32_t nb = len > 12u ? (len - 1u) / 12u : 0u;
+#pragma unroll
+        for (int k = 0; k < kMaxBlocks; k++) {
+            if ((uint32_t)k < nb) {
+                a += W(3 * k);
+                b += W(3 * k + 1);
+                c += W(3 * k + 2);
+                NC_JENKINS_MIX(a, b, c);
+            }
+        }
+        uint32_t wa = W(0), wb = W(1), wc = W(2);
+#pragma unroll
+        for (int k = 1; k <= kMaxBlocks; k++) {
+            if (nb == (uint32_t)k) {
+                wa = W(3 * k);
+                wb = W(3 * k + 1);
+                wc = W(3 * k + 2);
+            }
+        }
+        const uint32_t n = len - 12u * nb; /* 1..12 */
+        auto keep = [](uint32_t w, uint32_t m) { return m >= 4u ? w : (w & (0xffffffffu >> (32u - 8u * m))); };
+        a += keep(wa, n);
+        if (n > 4u) b += keep(wb, n - 4u);
+        if (n > 8u) c += keep(wc, n - 8u);
+        NC_JENKINS_FINAL(a, b, c);
+        return len == 0u ? init : c; /* nc_jenkins.c:121 */
+    } else {
+        const uint32_t nw = len >> 2, rem = len & 3u;
+        uint32_t h = MODE == NC_GPUHASH_MURMUR ? nc_murmur_init(len) : 0u;
+        uint32_t tw = W(0);
+#pragma unroll
+        for (int t = 0; t < NW; t++) {
+            if ((uint32_t)t < nw) h = MODE == NC_GPUHASH_MURMUR ? nc_murmur_word(h, W(t)) : nc_hsieh_word(h, W(t));
+            if (nw == (uint32_t)t + 1u) tw = W(t + 1);
+        }
+        if constexpr (MODE == NC_GPUHASH_MURMUR) return nc_murmur_final(nc_murmur_tail(h, tw, rem));
+        else return len == 0u ? 0u : nc_hsieh_final(nc_hsieh_tail(h, tw, rem)); /* nc_hsieh.c:44 */
+    }
+}
+
 /* the first nb (per lane, <= 16 * NC) key bytes of words d[0 .. NC); the crcs
  * take NW words (slicing-by-4NW, tables in R copies) per dependent step where
  * the whole group belongs to the key */
@@ -391,9 +455,13 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_short_kernel(const uint8_
                 jbad = j;
                 break;
             }
-            const uint32_t h = short_step<MODE, NC, NW, R>(init_state<MODE>(), dat[q], (int32_t)len, tab, lane4);
+            uint32_t hv;
+            if constexpr (is_word_mode<MODE>())
+                hv = short_words<MODE, NC>(dat[q], len);
+            else
+                hv = final_state<MODE>(short_step<MODE, NC, NW, R>(init_state<MODE>(), dat[q], (int32_t)len, tab, lane4));
             const rsrc_t rout = make_rsrc(out + k0, 4u * nv); /* lanes past the batch: dropped */
-            __builtin_amdgcn_raw_buffer_store_b32(final_state<MODE>(h), rout, (int)(lane * 4u), 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(hv, rout, (int)(lane * 4u), 0, kAuxNt);
         }
     }
     /* tiles jbad .. n - 1 (only when a key was longer than the shape said),
@@ -407,6 +475,12 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_short_kernel(const uint8_
         const rsrc_t r = make_rsrc(keys + s0, kbytes - s0);
         const uint32_t vo = o.s - (uint32_t)s0;
         int32_t rem = lane < nv ? (int32_t)(o.e - o.s) : 0;
+        if constexpr (is_word_mode<MODE>()) { /* byte loads, one lane per key (nc_hash_key.h) */
+            const uint32_t hw = lane < nv ? nc_key_hash(MODE, keys + s0 + vo, (uint64_t)rem, nullptr, nullptr) : 0u;
+            const rsrc_t rw = make_rsrc(out + k0, 4u * nv);
+            __builtin_amdgcn_raw_buffer_store_b32(hw, rw, (int)(lane * 4u), 0, kAuxNt);
+            continue;
+        }
         uint32_t h = init_state<MODE>();
         for (uint32_t b = 0; __ballot(rem > 0) != 0ull; b++) {
             u32x4 d4[4];
@@ -491,6 +565,8 @@ template <int MODE, int NC>
 hipError_t launch_short(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
                         hipStream_t stream, int var)
 {
+    /* jenkins: one tile ahead only (deeper, hipcc spills its mix state) */
+    if constexpr (MODE == NC_GPUHASH_JENKINS) return launch_short_d<MODE, NC, 2>(d_keys, d_off, nkeys, d_out, stream, var);
     switch (var & 3) {
     case 1: return launch_short_d<MODE, NC, 2>(d_keys, d_off, nkeys, d_out, stream, var);
     case 2: return launch_short_d<MODE, NC, 4>(d_keys, d_off, nkeys, d_out, stream, var);
@@ -550,6 +626,9 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
         if (max_len <= 16u) return launch_short<MODE, 1>(d_keys, d_off, nkeys, d_out, stream, var);
         return launch_short<MODE, 2>(d_keys, d_off, nkeys, d_out, stream, var);
     }
+    if constexpr (is_word_mode<MODE>()) {
+        return hipErrorInvalidValue; /* the word modes run on the short-key kernel only */
+    } else {
     if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_CRC32) {
         if (var & 64) return launch_opt<MODE, kOptNoHash>(d_keys, d_off, nkeys, d_out, stream, var);
     }
@@ -557,6 +636,7 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
         if (var & 32) return launch_opt<MODE, kOptS8>(d_keys, d_off, nkeys, d_out, stream, var);
     }
     return launch_opt<MODE, 0>(d_keys, d_off, nkeys, d_out, stream, var);
+    }
 }
 
 /* the byte-serial modes on the direct pipeline; var: bits 0-1 tiles per wave
@@ -564,6 +644,12 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
  * tiles interleaved over the grid (else consecutive), bit 4 (with 2 and 3)
  * eight-wave workgroups, one per CU, bits 5-7 as launch_mode. max_len: the
  * caller's longest key (its shape; 0xffffffff unknown). nkeys < 2^32. */
+/* hsieh, murmur, jenkins: the short-key kernel only (var bit 7, max_len <= 32) */
+bool supports_short_words(int mode)
+{
+    return mode == NC_GPUHASH_HSIEH || mode == NC_GPUHASH_MURMUR || mode == NC_GPUHASH_JENKINS;
+}
+
 bool supports(int mode)
 {
     switch (mode) {
@@ -593,6 +679,9 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
     case NC_GPUHASH_FNV1A_64: return launch_mode<NC_GPUHASH_FNV1A_64>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
     case NC_GPUHASH_FNV1_32: return launch_mode<NC_GPUHASH_FNV1_32>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
     case NC_GPUHASH_FNV1A_32: return launch_mode<NC_GPUHASH_FNV1A_32>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
+    case NC_GPUHASH_HSIEH: return launch_mode<NC_GPUHASH_HSIEH>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
+    case NC_GPUHASH_MURMUR: return launch_mode<NC_GPUHASH_MURMUR>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
+    case NC_GPUHASH_JENKINS: return launch_mode<NC_GPUHASH_JENKINS>(d_keys, d_off, nkeys, d_out, stream, var, max_len);
     default: return hipErrorInvalidValue;
     }
 }

@@ -1889,6 +1889,8 @@ hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, 
 namespace nc_bytes {
 /* the byte-serial modes on the direct pipeline (nc_bytes_kernels.hip) */
 bool supports(int mode);
+/* hsieh, murmur, jenkins on its short-key kernel only */
+bool supports_short_words(int mode);
 hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
                   hipStream_t stream, int var, uint32_t max_len);
 } // namespace nc_bytes
@@ -2445,6 +2447,12 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
     if (fixed && mean >= 20u && sh->max_len <= 32u &&
         (mode == NC_GPUHASH_CRC32 || mode == NC_GPUHASH_CRC32A || mode == NC_GPUHASH_ONE_AT_A_TIME))
         return kVarDirect | kVarDirectShort | (2 << 20) | (mode == NC_GPUHASH_ONE_AT_A_TIME ? 0 : (1 << 22));
+    /* ... and murmur, one tile in flight: 0.541 -> 0.517 ms (hsieh keeps the
+     * ring, 0.509 vs 0.521; jenkins the register-staged pipeline, 0.601 vs
+     * 0.648: its mix chain needs more than two waves per SIMD;
+     * profiles/r05_c3_short_words_ab.jsonl) */
+    if (fixed && mean >= 20u && sh->max_len <= 32u && mode == NC_GPUHASH_MURMUR)
+        return kVarDirect | kVarDirectShort | (1 << 20);
     /* fixed-length short keys: the crcs' slicing-by-4 tables on the direct
      * pipeline (C3: 0.70 -> 0.61 ms); varying lengths keep the length-grouped
      * workgroup pipelines (a direct wave runs to its longest key) */
@@ -2510,7 +2518,9 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
             return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream,
                                   ((var >> 20) & 15) | ((var & kVarMd5PadTab) != 0 ? 16 : 0), fl);
         }
-        if (nc_bytes::supports(mode))
+        const bool short_words = (var & kVarDirectShort) != 0 && nc_bytes::supports_short_words(mode) &&
+                                 shape != nullptr && nkeys != 0 && shape->max_len <= 32u;
+        if (nc_bytes::supports(mode) || short_words)
             return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream,
                                     ((var >> 20) & 15) | ((var & kVarDirect8) != 0 ? 16 : 0) |
                                         ((var & kVarDirectS8) != 0 ? 32 : 0) | ((var & kVarDirectNoHash) != 0 ? 64 : 0) |
