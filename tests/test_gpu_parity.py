@@ -423,14 +423,16 @@ def test_direct_short_keys(gpu, oracle, depth_bits, slice_bits):
                                  (1 << 19) | (11 << 20), (1 << 19) | (14 << 20), (1 << 19) | (9 << 20),
                                  (1 << 19) | (14 << 20) | (1 << 12), (1 << 19) | (10 << 20) | (1 << 13),
                                  (1 << 19) | (14 << 20) | (1 << 13), (1 << 19) | (1 << 13), (1 << 19) | (1 << 15),
-                                 (1 << 19) | (8 << 20) | (1 << 15)],
+                                 (1 << 19) | (8 << 20) | (1 << 15), (1 << 19) | (14 << 20) | (1 << 12) | (1 << 10)],
                          ids=["direct", "lines", "il16", "il32", "il64", "lines_il32", "il8", "lines_il32_w8",
-                              "il32_s8", "lines_il32_s8", "direct_s8", "direct_padtab", "il16_padtab"])
+                              "il32_s8", "lines_il32_s8", "direct_s8", "direct_padtab", "il16_padtab",
+                              "pairs_il32_w8"])
 def test_direct_ragged_tiles(gpu, oracle, var):
     """The direct per-lane pipelines (md5 and the byte-serial modes; the other
     modes take their default pipeline), consecutive or grid-interleaved tiles
     per wave, the byte modes' eight-wave line-image workgroups (bit 12), the
-    crcs' slicing-by-8 tables (bit 13), md5's LDS padding selectors (bit 15), on
+    crcs' slicing-by-8 tables (bit 13), md5's LDS padding selectors (bit 15),
+    the eight-wave line image in rounds of two lines (bit 10), on
     batch sizes around the 64-key tile and the per-workgroup tile
     count, with empty keys, one-block, multi-block and padding-only-block keys,
     a misaligned key buffer, against the oracle."""

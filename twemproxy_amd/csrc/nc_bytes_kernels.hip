@@ -69,6 +69,7 @@ constexpr uint32_t kCopies = 8;
 constexpr uint32_t kTabWords = nc_slice::table_words<kCopies>();
 constexpr int kOptS8 = 1;     /* slicing-by-8 crcs */
 constexpr int kOptNoHash = 2; /* DIAGNOSTIC: xor of the key's words, not a hash (the pipeline's memory side) */
+constexpr int kOptPairs = 16; /* the line image's rounds of two lines (256 B per key; eight-wave workgroups) */
 
 template <int MODE, bool LDS, int OPT>
 struct Tab {
@@ -172,12 +173,14 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
                                                               uint32_t chunk)
 {
     /* a round consumes RB bytes of every key: one 64-byte block from
-     * registers, or (LDS) one 128-byte line from the image */
-    constexpr uint32_t RB = LDS ? 128u : 64u;
+     * registers, (LDS) one 128-byte line from the image, or (PAIRS) two */
+    constexpr bool PAIRS = LDS && (OPT & kOptPairs) != 0;
+    constexpr uint32_t RB = PAIRS ? 256u : (LDS ? 128u : 64u);
+    constexpr uint32_t kImg = PAIRS ? 2u * kLineImage : kLineImage;
     using TB = Tab<MODE, LDS, OPT>;
     constexpr bool kTable = has_table<MODE>() && (OPT & kOptNoHash) == 0;
     __shared__ uint32_t tab[kTable ? TB::kWords : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? WAVES * kLineImage : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t kbuf[LDS ? WAVES * kImg : 16];
     if constexpr (kTable) {
         nc_slice::fill<MODE, TB::R, TB::NT>(tab, threadIdx.x, 64u * WAVES);
         __syncthreads();
@@ -191,12 +194,13 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
     if (tile >= tlast) return;
     Walker<IL> wk;
     wk.init(keys, off, nkeys, tiles, lane);
-    uint8_t *const img = kbuf + (LDS ? wave * kLineImage : 0u);
+    uint8_t *const img = kbuf + (LDS ? wave * kImg : 0u);
 
     TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
     Offs no = wk.load_off(tile + 1u);
     u32x4 da[4], db[4];
-    if constexpr (LDS) wk.dma_lines(cur_t, 0u, img);
+    if constexpr (PAIRS) wk.dma_pairs(cur_t, 0u, img);
+    else if constexpr (LDS) wk.dma_lines(cur_t, 0u, img);
     else wk.load_regs(cur_t, 0u, da);
     uint32_t b = 0;
     uint32_t h = init_state<MODE>();
@@ -206,7 +210,12 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
     auto round = [&](u32x4 (&cur)[4], u32x4 (&nxt)[4]) __attribute__((always_inline)) {
         const bool more = __ballot(cur_t.valid && cur_t.len > RB * (b + 1u)) != 0ull;
         const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
-        if constexpr (LDS) {
+        u32x4 dp[PAIRS ? 16 : 1];
+        if constexpr (PAIRS) {
+            wk.read_pairs(img, dp);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the image's reads are done */
+            wk.dma_pairs(more ? cur_t : nxt_t, more ? b + 1u : 0u, img);
+        } else if constexpr (LDS) {
             wk.read_lines(img, cur, nxt);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the image's reads are done */
             wk.dma_lines(more ? cur_t : nxt_t, more ? b + 1u : 0u, img);
@@ -219,9 +228,17 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
 
         const int32_t rem = (int32_t)cur_t.len - (int32_t)RB * (int32_t)b;
         if (cur_t.valid && (rem > 0 || (b == 0u && cur_t.len == 0u))) {
-            h = block_step<MODE, LDS, OPT>(h, cur, rem, tab, lane4);
-            if constexpr (LDS) {
-                if (rem > 64) h = block_step<MODE, LDS, OPT>(h, nxt, rem - 64, tab, lane4);
+            if constexpr (PAIRS) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const u32x4 d4[4] = {dp[4 * q], dp[4 * q + 1], dp[4 * q + 2], dp[4 * q + 3]};
+                    if (q == 0 || rem > 64 * q) h = block_step<MODE, LDS, OPT>(h, d4, rem - 64 * q, tab, lane4);
+                }
+            } else {
+                h = block_step<MODE, LDS, OPT>(h, cur, rem, tab, lane4);
+                if constexpr (LDS) {
+                    if (rem > 64) h = block_step<MODE, LDS, OPT>(h, nxt, rem - 64, tab, lane4);
+                }
             }
             if (rem <= (int32_t)RB) {
                 const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
@@ -590,6 +607,13 @@ hipError_t launch_opt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nke
          * keeps a second out): half the concurrent key streams */
         const uint64_t grid8 = (ntiles + 8u * chunk - 1u) / (8u * chunk);
         if (grid8 > 0x7fffffffu) return hipErrorInvalidValue;
+        if constexpr (!has_table<MODE>() && (OPT & kOptNoHash) == 0) {
+            if (var & 256) { /* two lines per round: 16 KiB images, 128 KiB per workgroup, one per CU */
+                hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true, 8, OPT | kOptPairs>), dim3((unsigned)grid8),
+                                   dim3(512), 0, stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
+                return hipGetLastError();
+            }
+        }
         const uint32_t pad = has_table<MODE>() ? 0u : 40960u;
         if (pad)
             (void)hipFuncSetAttribute((const void *)nc_bytes_direct_kernel<MODE, true, true, 8, OPT>,
@@ -642,8 +666,10 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
 /* the byte-serial modes on the direct pipeline; var: bits 0-1 tiles per wave
  * (16, 8, 32, 64), bit 2 the LDS-DMA block image (long keys), bit 3 a wave's
  * tiles interleaved over the grid (else consecutive), bit 4 (with 2 and 3)
- * eight-wave workgroups, one per CU, bits 5-7 as launch_mode. max_len: the
- * caller's longest key (its shape; 0xffffffff unknown). nkeys < 2^32. */
+ * eight-wave workgroups, one per CU (bit 8 with them, no crc table: rounds
+ * of two lines, dma_pairs), bits 5-7 as launch_mode. max_len: the caller's
+ * longest key (its shape; 0xffffffff unknown). nkeys < 2^32. */
+
 /* hsieh, murmur, jenkins: the short-key kernel only (var bit 7, max_len <= 32) */
 bool supports_short_words(int mode)
 {

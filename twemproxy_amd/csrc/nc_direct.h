@@ -215,6 +215,39 @@ struct Walker {
         }
     }
 
+    /* Long keys, two whole lines per round: bytes [256b, 256b + 256) of the
+     * lanes' keys into a 16 KiB image (key k's 256 bytes at k * 256), for
+     * workgroups few enough to double the bytes in flight per wave (eight
+     * waves per CU: 128 KiB). Instruction i moves keys 4i .. 4i+3, sixteen
+     * lanes per key; chunk j of key k lands in slot j ^ (k & 15): every row
+     * starts on bank 0, so slot s sits on banks 4s .. 4s+3, and the 16 lanes
+     * of each ds_read_b128 lane group (MI355X_MICROARCH.md §LDS: k mod 16
+     * distinct within a group) read 16 distinct slots. */
+    __device__ __forceinline__ void dma_pairs(const TileKeys &t, uint32_t b, uint8_t *img) const
+    {
+        const rsrc_t r = make_rsrc(keys + t.s0, kbytes - t.s0);
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int key = 4 * i + (int)(lane >> 4);
+            const uint32_t j = (lane & 15u) ^ ((uint32_t)key & 15u); /* the global chunk for this slot */
+            const uint32_t vo = (uint32_t)__shfl((int)t.srel, key);
+            const int32_t rem = __shfl((int)t.len, key) - 256 * (int32_t)b;
+            if (rem > (int32_t)(16u * j))
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(img + 1024 * i),
+                                                          16, vo + 256u * b + 16u * j, 0, 0, 0);
+        }
+    }
+
+    /* this lane's 256 bytes from the pair image (see dma_pairs) */
+    __device__ __forceinline__ void read_pairs(const uint8_t *img, u32x4 (&d)[16]) const
+    {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint8_t *row = img + lane * 256u;
+        const uint32_t sw = lane & 15u;
+#pragma unroll
+        for (int c = 0; c < 16; c++) d[c] = *reinterpret_cast<const u32x4 *>(row + 16u * ((uint32_t)c ^ sw));
+    }
+
     /* this lane's 128 bytes from the line image (see dma_lines) */
     __device__ __forceinline__ void read_lines(const uint8_t *img, u32x4 (&d0)[4], u32x4 (&d1)[4]) const
     {

@@ -1941,7 +1941,8 @@ constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
 constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
 constexpr int kVarMd5PadTab = 1 << 15;    /* md5: padding selectors from an LDS table */
 constexpr int kVarDirectShort = 1 << 11;  /* byte modes, keys <= 32 B: eight waves per CU, tiles in flight */
-static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash | kVarMd5PadTab | kVarDirectShort) &
+constexpr int kVarDirectPairs = 1 << 10;  /* with kVarDirect8: the line image in rounds of two lines */
+static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash | kVarMd5PadTab | kVarDirectShort | kVarDirectPairs) &
                (kVarMd5Direct | (15 << 20) | kVarNoFixedLen | kVarWsort | kVarGsort | kVarNoPacked | (3 << 29))) == 0,
               "direct-pipeline options overlap the pipeline choice, its nibble or the server_idx bits");
 
@@ -2524,7 +2525,7 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
             return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream,
                                     ((var >> 20) & 15) | ((var & kVarDirect8) != 0 ? 16 : 0) |
                                         ((var & kVarDirectS8) != 0 ? 32 : 0) | ((var & kVarDirectNoHash) != 0 ? 64 : 0) |
-                                        ((var & kVarDirectShort) != 0 ? 128 : 0),
+                                        ((var & kVarDirectShort) != 0 ? 128 : 0) | ((var & kVarDirectPairs) != 0 ? 256 : 0),
                                     shape != nullptr && nkeys != 0 ? (uint32_t)shape->max_len : 0xffffffffu);
     }
     if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))
