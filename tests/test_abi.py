@@ -182,8 +182,9 @@ def test_auto_policy_choices():
     assert t.pick_variant("md5", n, (16 * n, 16, 16)) == DIRECT | PADTAB
     for name in ("crc32", "one_at_a_time", "crc16"):
         assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | IL32, name
-    for name in ("fnv1a_64", "fnv1_32"):  # eight-wave workgroups, one per CU
-        assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | IL32 | (1 << 12), name
+    for name in ("fnv1a_64", "fnv1_32"):  # eight-wave workgroups, one per CU, rounds of two lines
+        assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | IL32 | (1 << 12) | (1 << 10), name
+        assert t.pick_variant(name, n >> 3, (128 * (n >> 3), 128, 128)) == DIRECT | DIRECT_LDS | IL32 | (1 << 12), name
     assert t.pick_variant("md5", n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | (8 << 20)
     assert t.pick_variant("md5", n >> 3, (128 * (n >> 3), 128, 128)) == DIRECT | DIRECT_LDS | (8 << 20)
     assert t.pick_variant("murmur", n >> 3, (256 * (n >> 3), 256, 256)) == RING4

@@ -608,7 +608,11 @@ hipError_t launch_opt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nke
         const uint64_t grid8 = (ntiles + 8u * chunk - 1u) / (8u * chunk);
         if (grid8 > 0x7fffffffu) return hipErrorInvalidValue;
         if constexpr (!has_table<MODE>() && (OPT & kOptNoHash) == 0) {
-            if (var & 256) { /* two lines per round: 16 KiB images, 128 KiB per workgroup, one per CU */
+            /* two lines per round: 16 KiB images, 128 KiB per workgroup, one per
+             * CU (the crcs' table does not fit beside them at 16 waves, and at
+             * eight their lookups run 2.08-2.24 ms on the C4 shard against
+             * 1.84, profiles/r05_c4_pairs_crc_ab.jsonl) */
+            if (var & 256) {
                 hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true, 8, OPT | kOptPairs>), dim3((unsigned)grid8),
                                    dim3(512), 0, stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
                 return hipGetLastError();

@@ -2430,12 +2430,17 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
          * the fnvs at half the resident waves, 1.55 -> 1.52 (their streams
          * contend for HBM; crc32's table lookups need the waves: 1.83 -> 2.22,
          * profiles/r04_lines_occupancy_ab.jsonl) */
+        /* ... and, from 160-byte keys on average, the fnvs' rounds take two
+         * lines of every key (twice the bytes in flight per wave): C4 shard
+         * fnv1a_64 1.622 -> 1.542 ms, fnv1_32 1.625 -> 1.542, uniform
+         * 80-400 B 1.241 -> 1.129; fixed 128 B keys lose (0.429 -> 0.491: half
+         * of each round's image idle) (profiles/r05_c4_pairs_ab.jsonl,
+         * r05_c4_pairs_crc_ab.jsonl) */
+        const bool fnv = mode == NC_GPUHASH_FNV1_64 || mode == NC_GPUHASH_FNV1A_64 || mode == NC_GPUHASH_FNV1_32 ||
+                         mode == NC_GPUHASH_FNV1A_32;
         if (direct_bytes)
             return kVarDirect | kVarDirectLds | kVarDirectIl32 |
-                   (mode == NC_GPUHASH_FNV1_64 || mode == NC_GPUHASH_FNV1A_64 || mode == NC_GPUHASH_FNV1_32 ||
-                            mode == NC_GPUHASH_FNV1A_32
-                        ? kVarDirect8
-                        : 0);
+                   (fnv ? kVarDirect8 | (mean >= 160u ? kVarDirectPairs : 0) : 0);
         if (mode == NC_GPUHASH_HSIEH) return kVarRingP5;
         return kVarRingP4;
     }
