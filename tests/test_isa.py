@@ -77,6 +77,22 @@ def test_no_scratch_in_hash_kernels(asm_file):
         assert m and m[0].split()[-1] == "0", f"{name} uses scratch: {m}"
 
 
+@pytest.mark.parametrize("src,prefix", [("nc_bytes_kernels.s", "nc_bytes_"), ("nc_md5_kernels.s", "nc_md5_")])
+def test_no_scratch_in_direct_kernels(asm_file, src, prefix):
+    """the direct family (the byte modes' direct, line and short-key kernels,
+    md5's direct and line kernels): no instantiation spills to scratch"""
+    text = open(os.path.join(os.path.dirname(asm_file), src)).read()
+    n = 0
+    for block in text.split(".amdhsa_kernel ")[1:]:
+        name = block.split()[0]
+        if prefix not in name:
+            continue
+        n += 1
+        m = [l for l in block.splitlines() if ".amdhsa_private_segment_fixed_size" in l]
+        assert m and m[0].split()[-1] == "0", f"{name} uses scratch: {m}"
+    assert n > 10
+
+
 def test_lds_fits_eight_workgroups(asm_file):
     """Every workgroup-pipeline kernel leaves room for eight workgroups per
     CU (160 KiB of LDS), the grouped pipeline's three-slab form for seven

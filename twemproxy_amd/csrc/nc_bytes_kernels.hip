@@ -583,11 +583,14 @@ hipError_t launch_short(const uint8_t *d_keys, const uint64_t *d_off, uint64_t n
                         hipStream_t stream, int var)
 {
     /* jenkins: one tile ahead only (deeper, hipcc spills its mix state) */
-    if constexpr (MODE == NC_GPUHASH_JENKINS) return launch_short_d<MODE, NC, 2>(d_keys, d_off, nkeys, d_out, stream, var);
-    switch (var & 3) {
-    case 1: return launch_short_d<MODE, NC, 2>(d_keys, d_off, nkeys, d_out, stream, var);
-    case 2: return launch_short_d<MODE, NC, 4>(d_keys, d_off, nkeys, d_out, stream, var);
-    default: return launch_short_d<MODE, NC, 3>(d_keys, d_off, nkeys, d_out, stream, var);
+    if constexpr (MODE == NC_GPUHASH_JENKINS) {
+        return launch_short_d<MODE, NC, 2>(d_keys, d_off, nkeys, d_out, stream, var);
+    } else {
+        switch (var & 3) {
+        case 1: return launch_short_d<MODE, NC, 2>(d_keys, d_off, nkeys, d_out, stream, var);
+        case 2: return launch_short_d<MODE, NC, 4>(d_keys, d_off, nkeys, d_out, stream, var);
+        default: return launch_short_d<MODE, NC, 3>(d_keys, d_off, nkeys, d_out, stream, var);
+        }
     }
 }
 

@@ -314,7 +314,18 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
             return std::array<uint32_t, 4>{v[0], v[1], v[2], v[3]};
         };
         if (!fl_tile) { /* (a fixed-length tile, FL <= 48, has no tail keys) */
-            const std::array<uint32_t, 4> v = b == 0u ? gen(std::true_type{}) : gen(std::false_type{});
+            std::array<uint32_t, 4> v;
+            if constexpr (FL > 0) { /* a fixed-length kernel's odd tile: one step copy (two spill at 64 VGPRs) */
+                if (b == 0u) {
+                    st[0] = NC_MD5_A0;
+                    st[1] = NC_MD5_B0;
+                    st[2] = NC_MD5_C0;
+                    st[3] = NC_MD5_D0;
+                }
+                v = gen(std::false_type{});
+            } else {
+                v = b == 0u ? gen(std::true_type{}) : gen(std::false_type{});
+            }
             /* keys whose last data block could not take the length (or empty
              * keys) queue their state for a data-free tail block */
 
