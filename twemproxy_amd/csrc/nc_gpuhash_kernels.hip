@@ -254,11 +254,11 @@ __device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const 
 
 /* The same over a PACKED LDS continuum, one word per point: the value's top
  * 24 bits over the server index (w = v & ~255 | server, pools of <= 256
- * servers), followed by eight 0xffffffff sentinels (never below a hash's top
+ * servers), followed by four 0xffffffff sentinels (never below a hash's top
  * 24 bits, so a scan stops at them without bounds checks). 4 bytes a point
  * keep a 1280-point pool inside the grouped pipeline's four workgroups per
  * CU. A 512-entry u16 bucket index over the hash's top 9 bits (~2.5 points a
- * bucket) starts a SCAN four points at a time (one aligned ds_read_b128): most keys
+ * bucket) starts a SCAN four points at a time (two ds_read2_b32): most keys
  * resolve in two LDS round trips. The scan compares h >> 8; only when the
  * found point shares h's top 24 bits is the answer ambiguous, and that lane
  * walks the run of such points comparing full values from the continuum in
@@ -269,20 +269,16 @@ __device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, co
 {
     const uint32_t hb = h & ~0xffu; /* w >> 8 < h >> 8  <=>  w < hb */
     /* clamped: an unsorted continuum (a caller error) could leave a bucket
-     * unwritten; from at most n the scan still ends at the sentinels. The
-     * scan reads aligned quads (one ds_read_b128 each) from the quad that
-     * holds the bucket's first point: the points before it in that quad lie
-     * below the bucket, hence below h, and only add to k */
-    uint32_t lo = min((uint32_t)bkt16[h >> 23], n) & ~3u;
+     * unwritten; from at most n the scan still ends at the sentinels */
+    uint32_t lo = min((uint32_t)bkt16[h >> 23], n);
     uint32_t pos, cand;
     for (;;) {
-        typedef unsigned int q4 __attribute__((ext_vector_type(4)));
-        const q4 c = *reinterpret_cast<const q4 *>(w + lo);
+        const uint32_t c0 = w[lo], c1 = w[lo + 1u], c2 = w[lo + 2u], c3 = w[lo + 3u];
         /* sorted words: those below h come first */
-        const uint32_t k = (uint32_t)(c.x < hb) + (uint32_t)(c.y < hb) + (uint32_t)(c.z < hb) + (uint32_t)(c.w < hb);
+        const uint32_t k = (uint32_t)(c0 < hb) + (uint32_t)(c1 < hb) + (uint32_t)(c2 < hb) + (uint32_t)(c3 < hb);
         if (k < 4u) {
             pos = lo + k;
-            cand = k == 0u ? c.x : (k == 1u ? c.y : (k == 2u ? c.z : c.w));
+            cand = k == 0u ? c0 : (k == 1u ? c1 : (k == 2u ? c2 : c3));
             break;
         }
         lo += 4u; /* all four below h */
@@ -967,7 +963,7 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
         }
     } else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked) {
         pw0 = (dist.cont[1] & ~0xffu) | (dist.cont[0] & 0xffu); /* point 0, the wrap's answer */
-        for (uint32_t i = t; i < dist.ncont + 8u; i += TK) /* + sentinels to the end of the last aligned quad */
+        for (uint32_t i = t; i < dist.ncont + 4u; i += TK) /* + four sentinels */
             gs_cont[i] = i < dist.ncont ? (dist.cont[2u * i + 1u] & ~0xffu) | (dist.cont[2u * i] & 0xffu) : ~0u;
         /* the u16[512] bucket starts (in the table's 1 KiB) from the staged
          * words, not by 512 binary searches over global memory (eleven
@@ -1935,7 +1931,7 @@ constexpr int kVarGsortCs = 1 << 27; /* its hashes stored once per tile, 16 byte
 constexpr int kVarGsort512 = 1 << 26; /* with kVarGsortCs: 512-key tiles, eight waves (length octiles) */
 constexpr int kVarGsortIssue = 1 << 28; /* A/B: the grouped tile's DMAs issued before the previous tile's store */
 constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline stages in LDS (5 B each) */
-constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 8 sentinels), beside four 512-key
+constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 4 sentinels), beside four 512-key
                                             workgroups per CU */
 constexpr int kVarNoPacked = 1 << 27; /* server_idx A/B: the 5-byte LDS continuum even where the packed one fits */
 /* direct byte kernels' options beyond bits 20-23, in bits only the ring
@@ -2343,8 +2339,8 @@ hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t 
                      * tiles' budget: four workgroups per CU, as without a
                      * dispatch */
                     const int sets = (d.gs_var & (3 << 21)) != 0 ? d.gs_var : (d.gs_var | (2 << 21));
-                    constexpr int kR = (kLdsPackedMax + 8) * 4;
-                    const size_t dyn = ((size_t)d.ncont + 8u) * 4u;
+                    constexpr int kR = (kLdsPackedMax + 4) * 4;
+                    const size_t dyn = ((size_t)d.ncont + 4u) * 4u;
                     if constexpr (MODE == NC_GPUHASH_FNV1A_64) { /* DIAGNOSTIC (tuning bits 19 / 20): what the
                                                                     dispatch costs — no hash_tag code / no search */
                         switch ((d.gs_var >> 19) & 3) {
