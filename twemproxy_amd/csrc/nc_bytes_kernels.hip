@@ -540,11 +540,10 @@ static int num_cus()
  * var bits 0-1 the depth (3, 2, 4 tiles: 2, 1, 3 ahead), bits 2-3 the crcs'
  * tables (slicing-by-4 in 8 copies, by-8 in 8 copies, by-16 in 8, by-4 in 32:
  * one copy per lane of a ds_read_b32 lane group, conflict-free) */
-template <int MODE, int NC, int DEPTH, int NW, uint32_t R>
+template <int MODE, int NC, int DEPTH, int NW, uint32_t R, int kW = 8>
 hipError_t launch_short_t(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
                           hipStream_t stream)
 {
-    constexpr int kW = 8;
     const uint64_t ntiles = (nkeys + 63u) / 64u;
     uint64_t grid = (uint64_t)num_cus();
     const uint64_t need = (ntiles + kW - 1u) / kW;
@@ -569,12 +568,16 @@ hipError_t launch_short_d(const uint8_t *d_keys, const uint64_t *d_off, uint64_t
 {
     if constexpr (has_table<MODE>()) {
         switch ((var >> 2) & 3) {
-        case 1: return launch_short_t<MODE, NC, DEPTH, 2, 8>(d_keys, d_off, nkeys, d_out, stream);
+        case 1:
+            if (var & 16) return launch_short_t<MODE, NC, DEPTH, 2, 8, 16>(d_keys, d_off, nkeys, d_out, stream);
+            return launch_short_t<MODE, NC, DEPTH, 2, 8>(d_keys, d_off, nkeys, d_out, stream);
         case 2: return launch_short_t<MODE, NC, DEPTH, 4, 8>(d_keys, d_off, nkeys, d_out, stream);
         case 3: return launch_short_t<MODE, NC, DEPTH, 1, 32>(d_keys, d_off, nkeys, d_out, stream);
         default: break;
         }
     }
+    /* var bit 4: sixteen waves per CU (one 1024-thread workgroup) */
+    if (var & 16) return launch_short_t<MODE, NC, DEPTH, 1, 8, 16>(d_keys, d_off, nkeys, d_out, stream);
     return launch_short_t<MODE, NC, DEPTH, 1, 8>(d_keys, d_off, nkeys, d_out, stream);
 }
 
