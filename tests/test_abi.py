@@ -168,14 +168,15 @@ def test_auto_policy_choices():
     for name in ("fnv1_64", "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == RING5, name
     SHORT = 1 << 11  # the short-key kernel (eight waves per CU); bits 20-21 depth, 22-23 the crc tables
-    assert t.pick_variant("crc16", n, (32 * n, 32, 32)) == DIRECT | IL32
+    for name in ("crc16", "jenkins"):  # sixteen waves per CU (variant bit 12)
+        assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT | SHORT | (1 << 12), name
     for name in ("crc32", "crc32a"):  # three tiles in flight, slicing-by-8
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT | SHORT | (2 << 20) | (1 << 22), name
     assert t.pick_variant("one_at_a_time", n, (32 * n, 32, 32)) == DIRECT | SHORT | (2 << 20)
     assert t.pick_variant("murmur", n, (32 * n, 32, 32)) == DIRECT | SHORT | (1 << 20)  # one tile in flight
     assert t.pick_variant("murmur", n, (36 * n, 36, 36)) == RING5  # longer than 32 B
     assert t.pick_variant("crc32", n, (36 * n, 36, 36)) == DIRECT | IL32  # longer than 32 B
-    assert t.pick_variant("jenkins", n, (32 * n, 32, 32)) == RS
+    assert t.pick_variant("jenkins", n, (36 * n, 36, 36)) == RS
     assert t.pick_variant("md5", n, (32 * n, 32, 32)) == DIRECT | PADTAB
     # short fixed, long keys (C4)
     assert t.pick_variant("fnv1a_64", n, (8 * n, 8, 8)) == WG

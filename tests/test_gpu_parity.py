@@ -380,9 +380,9 @@ def test_wave_ring_crc_sliced(gpu, oracle, var):
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
 
 
-@pytest.mark.parametrize("depth_bits,slice_bits", [(0, 0), (1, 1), (2, 2), (0, 3)],
-                         ids=["ahead2-s4", "ahead1-s8", "ahead3-s16", "ahead2-s4r32"])
-def test_direct_short_keys(gpu, oracle, depth_bits, slice_bits):
+@pytest.mark.parametrize("depth_bits,slice_bits,w16", [(0, 0, 0), (1, 1, 0), (2, 2, 0), (0, 3, 0), (0, 0, 1), (2, 1, 1)],
+                         ids=["ahead2-s4", "ahead1-s8", "ahead3-s16", "ahead2-s4r32", "ahead2-s4-w16", "ahead3-s8-w16"])
+def test_direct_short_keys(gpu, oracle, depth_bits, slice_bits, w16):
     """The short-key kernel (variant bit 11 with the direct
     pipeline: keys of at most 16 or 32 bytes by the caller's shape, eight
     waves per CU on a persistent grid, 1-3 tiles in flight per wave) on
@@ -391,8 +391,8 @@ def test_direct_short_keys(gpu, oracle, depth_bits, slice_bits):
     (from that tile on, the slow loop from global memory), against the
     oracle, for the byte modes and the word modes (hsieh, murmur, jenkins).
     The crcs by slicing-by-4, -8 and -16 tables (variant bits 22-23;
-    by-4 also in 32 copies)."""
-    var = (1 << 19) | (1 << 11) | (depth_bits << 20) | (slice_bits << 22)
+    by-4 also in 32 copies); eight or sixteen waves per CU (bit 12)."""
+    var = (1 << 19) | (1 << 11) | (depth_bits << 20) | (slice_bits << 22) | (w16 << 12)
     L.lib().nc_gpuhash_set_tuning(0, 0, var)
     import torch
 

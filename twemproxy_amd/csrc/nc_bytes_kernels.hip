@@ -473,10 +473,11 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_short_kernel(const uint8_
                 break;
             }
             uint32_t hv;
-            if constexpr (is_word_mode<MODE>())
+            if constexpr (is_word_mode<MODE>()) {
                 hv = short_words<MODE, NC>(dat[q], len);
-            else
+            } else {
                 hv = final_state<MODE>(short_step<MODE, NC, NW, R>(init_state<MODE>(), dat[q], (int32_t)len, tab, lane4));
+            }
             const rsrc_t rout = make_rsrc(out + k0, 4u * nv); /* lanes past the batch: dropped */
             __builtin_amdgcn_raw_buffer_store_b32(hv, rout, (int)(lane * 4u), 0, kAuxNt);
         }
