@@ -69,7 +69,12 @@ rstatus_t nc_gpuhash_time_device_shaped(int mode, const uint8_t *d_keys, const u
  * pipeline as an explicit choice; bit 17: length-grouped tiles, as sort = 1;
  * bit 18: workgroup pipelines launch three resident sets of workgroups;
  * bit 19: the direct per-lane pipeline (md5 and the byte-serial modes), bits
- * 20-23 its options (tiles per wave, 128-byte line image, grid interleave);
+ * 20-23 its options (tiles per wave, 128-byte line image, grid interleave),
+ * and with it: bit 10 rounds of two lines (eight-wave line kernel, no crc),
+ * bit 11 the short-key kernel for keys <= 32 B by the shape (bits 20-21 its
+ * tiles in flight, 22-23 the crc tables; the word modes too), bit 12 eight-wave
+ * line workgroups or, with bit 11, sixteen waves per CU, bit 13 slicing-by-8
+ * crc tables, bit 14 DIAGNOSTIC no-hash build, bit 15 md5's LDS pad table;
  * bit 24: the wave-sorted pipeline (fnv x4, one_at_a_time), bits 20-21 its
  * tiles per wave, bit 22 DIAGNOSTIC no-hash build (fnv1a_64), bit 23 its
  * tiles interleaved over the grid; bit 25: the grouped workgroup pipeline
