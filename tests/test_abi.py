@@ -168,8 +168,8 @@ def test_auto_policy_choices():
     for name in ("fnv1_64", "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == RING5, name
     SHORT = 1 << 11  # the short-key kernel (eight waves per CU); bits 20-21 depth, 22-23 the crc tables
-    for name in ("crc16", "jenkins"):  # sixteen waves per CU (variant bit 12)
-        assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT | SHORT | (1 << 12), name
+    assert t.pick_variant("crc16", n, (32 * n, 32, 32)) == DIRECT | SHORT | (1 << 12)  # sixteen waves per CU
+    assert t.pick_variant("jenkins", n, (32 * n, 32, 32)) == RS
     for name in ("crc32", "crc32a"):  # three tiles in flight, slicing-by-8
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT | SHORT | (2 << 20) | (1 << 22), name
     assert t.pick_variant("one_at_a_time", n, (32 * n, 32, 32)) == DIRECT | SHORT | (2 << 20)

@@ -2459,12 +2459,13 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
      * profiles/r05_c3_short_words_ab.jsonl) */
     if (fixed && mean >= 20u && sh->max_len <= 32u && mode == NC_GPUHASH_MURMUR)
         return kVarDirect | kVarDirectShort | (1 << 20);
-    /* crc16 and jenkins at SIXTEEN waves per CU on the same kernel (their
-     * chains need the waves; crc16 slicing-by-4, two tiles in flight; jenkins
-     * one): crc16 0.575-0.577 -> 0.549-0.550 ms, jenkins 0.594-0.596 ->
-     * 0.565-0.587 (profiles/r05_c3_short16_ab.jsonl, r05_c3_crc16_fl32_ab.jsonl;
-     * crc32 ties, one_at_a_time loses 7 %) */
-    if (fixed && mean >= 20u && sh->max_len <= 32u && (mode == NC_GPUHASH_CRC16 || mode == NC_GPUHASH_JENKINS))
+    /* crc16 at SIXTEEN waves per CU on the same kernel (its chain needs the
+     * waves; slicing-by-4, two tiles in flight): 0.575-0.577 -> 0.549-0.550 ms
+     * (profiles/r05_c3_short16_ab.jsonl, r05_c3_crc16_fl32_ab.jsonl; crc32
+     * ties, one_at_a_time loses 7 %, jenkins ties the register-staged
+     * pipeline at 1.056 x the algorithmic bytes instead of 1.028,
+     * r05b_modes_c3.json, and keeps it) */
+    if (fixed && mean >= 20u && sh->max_len <= 32u && mode == NC_GPUHASH_CRC16)
         return kVarDirect | kVarDirectShort | kVarDirect8;
     /* fixed-length short keys: the crcs' slicing-by-4 tables on the direct
      * pipeline (C3: 0.70 -> 0.61 ms); varying lengths keep the length-grouped
