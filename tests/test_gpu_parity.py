@@ -275,7 +275,7 @@ def test_key_buffers_beyond_4gib(gpu):
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     try:
         for var in (0, 65536, 32, 128, 896, 2176, 1 << 19, (1 << 19) | (4 << 20), (1 << 19) | (14 << 20),
-                    (1 << 19) | (8 << 20), 1 << 24, 1 << 25):
+                    (1 << 19) | (8 << 20), 1 << 24, 1 << 25, (1 << 19) | (14 << 20) | (1 << 12) | (1 << 10)):
             L.lib().nc_gpuhash_set_tuning(0, 0, var)
             for name in ("md5", "crc32", "fnv1a_64"):
                 t.hash_batch_device(name, kd, od, out, shape=spec.shape(256 * n))
@@ -295,6 +295,37 @@ def test_key_buffers_beyond_4gib(gpu):
             hv = t.hash_key("fnv1a_64", host[i])
             p = int(np.searchsorted(vals, hv, side="left")) % 8
             assert int(g[i]) == p % 4, (shape, i)
+    del kd, od, out
+    torch.cuda.empty_cache()
+
+
+def test_short_keys_beyond_4gib(gpu):
+    """4.25 GiB of 32-byte keys (offsets past 2^31 and 2^32) through the
+    short-key kernel as the policy picks it (crc32, crc16, one_at_a_time,
+    murmur) and with its other shapes: sampled keys around both marks against
+    the per-key host symbols."""
+    import torch
+
+    spec = t.SynthSpec.fixed(6, 32)
+    n = (1 << 27) + (1 << 23)
+    kd, od = t.synth_device(spec, 0, n)
+    rng = np.random.default_rng(6)
+    sample = sorted({0, n - 1} | {(1 << 26) + d for d in (-1, 0, 1)} | {(1 << 27) + d for d in (-1, 0, 1)} |
+                    {int(x) for x in rng.integers(0, n, size=24)})
+    host = {i: t.synth_host(spec, i, 1)[0][:32].tobytes() for i in sample}
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    short = (1 << 19) | (1 << 11)
+    try:
+        for var in (0, short, short | (1 << 20) | (1 << 22), short | (2 << 20) | (2 << 22), short | (1 << 12)):
+            L.lib().nc_gpuhash_set_tuning(0, 0, var)
+            for name in ("crc32", "crc16", "one_at_a_time", "murmur", "jenkins"):
+                t.hash_batch_device(name, kd, od, out, shape=spec.shape(32 * n))
+                torch.cuda.synchronize()
+                h = out.cpu().numpy().view(np.uint32)
+                for i in sample:
+                    assert int(h[i]) == t.hash_key(name, host[i]), (var, name, i)
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
     del kd, od, out
     torch.cuda.empty_cache()
 
