@@ -280,3 +280,56 @@ def test_ketama_lookup_table(gpu, oracle, dist_fixture):
     finally:
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
 
+
+
+def test_ketama_packed_top_hashes(gpu, oracle):
+    """The packed LDS continuum ends in sentinels 0xffffff00 | point 0's
+    server: a key whose hash has its top 24 bits all ones stops on a sentinel
+    (or on a real point >= 0xffffff00) with the same top 24 bits and must
+    resolve on full values — the wrap to point 0 past the last point, or the
+    point itself. Keys with such fnv1a_64 hashes are found among 2^26 C2 keys
+    on the device (about four), padded with 64 Ki ordinary C2 keys so the
+    policy keeps the grouped pipeline; pools of 1,280 points (the packed
+    limit) with the last point below those hashes, at them and above them,
+    against the oracle's server_pool_idx."""
+    import torch
+
+    from twemproxy_amd import _lib as L
+
+    spec = t.CONFIGS["C2"]["spec"]
+    kd, od = t.synth_device(spec, 0, 1 << 26)
+    h = t.hash_batch_device("fnv1a_64", kd, od).cpu().numpy().view(np.uint32)
+    del kd, od
+    torch.cuda.empty_cache()
+    top = np.flatnonzero(h >= 0xffffff00)
+    assert top.size >= 1, "no key of 2^26 hashes to >= 0xffffff00"
+    special = []
+    for i in top:
+        k1, o1 = t.synth_host(spec, int(i), 1)
+        special.append(bytes(k1[int(o1[0]):int(o1[1])]))
+    hs = h[top].astype(np.int64)
+    keys, off = t.synth_host(spec, 7, 1 << 16)
+    ordinary = [bytes(keys[off[i]:off[i + 1]]) for i in range(off.size - 1)]
+    keyset = ordinary[:30000] + special + ordinary[30000:] + special
+    pk, po = t.pack_keys(keyset)
+    kd, od = to_dev(pk, po)
+    shape = t.shape_of(po)
+    assert (oracle.batch(6, pk, po)[30000:30000 + len(special)] >= 0xffffff00).all()
+    rng = np.random.default_rng(5)
+    base = np.sort(rng.integers(0, 0xff000000, size=1280 - 8, dtype=np.uint64))
+    pools = []
+    for tail in ([], list(hs - 1), list(hs), list(hs + 1), [0xffffff00, 0xffffffff], [0xffffff00] * 3):
+        v = np.sort(np.clip(np.concatenate([base, np.array(tail, np.int64)]), 0, 0xffffffff)).astype(np.uint32)
+        pools.append((v, rng.integers(0, 8, size=v.size).astype(np.uint32)))
+    try:
+        for vals, idx in pools:
+            cd = t.continuum_device(idx, vals)
+            want = oracle.server_idx_batch(6, 0, vals, idx, 8, None, pk, po)
+            for var in (0, 1 << 30, (1 << 30) | (1 << 27)):
+                L.lib().nc_gpuhash_set_tuning(0, 0, var)
+                got = t.server_idx_device(6, "ketama", kd, od, cd, 8, shape=shape)
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want,
+                                              err_msg=f"{vals[-3:]} var={var:#x}")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)

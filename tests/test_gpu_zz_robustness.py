@@ -25,7 +25,7 @@ def test_ketama_unsorted_continuum_terminates(gpu, npoints, var):
     """A continuum that is not sorted is a caller error (ketama_update sorts,
     src/hashkit/nc_ketama.c:198), but every ketama search must still end
     inside the continuum: bucket spans are clamped to n (bucket_span), and
-    the packed scan also stops at its four sentinels. The results are
+    the packed search also stops at its eight sentinels. The results are
     unspecified; the launch must return server indices."""
     import torch
 

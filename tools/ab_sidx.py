@@ -9,6 +9,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
@@ -22,7 +23,9 @@ PIPES = {"policy": 0, "ring": 1 << 28, "workgroup": 1 << 29, "grouped": 1 << 30,
          "grouped8": (1 << 30) | (3 << 21), "grouped_5b": (1 << 30) | (1 << 27),
          # DIAGNOSTIC (fnv1a_64, packed continuum): no hash_tag code / no search (outputs are hashes) / neither
          "diag_notag": (1 << 30) | (1 << 19), "diag_nosearch": (1 << 30) | (2 << 19),
-         "diag_bare": (1 << 30) | (3 << 19)}
+         "diag_bare": (1 << 30) | (3 << 19), "diag_bare_noprologue": (1 << 30) | (3 << 19) | (1 << 26),
+         # the plain hash of the same keys (hash_device, its own policy)
+         "plain_hash": None}
 GRIDS = {}  # name -> grid cap (--grids: workgroup pipeline at these caps)
 
 
@@ -34,6 +37,8 @@ def main():
     ap.add_argument("--tags", default="none")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--spinup", type=float, default=0.5, help="seconds of untimed launches before each entry "
+                    "(device clocks ramp up under load, as bench.py's SPINUP_S)")
     ap.add_argument("--grids", default="", help="comma-separated grid caps for extra workgroup entries")
     ap.add_argument("--pipes", default="", help="comma-separated subset of the pipeline names")
     ap.add_argument("--lib", default="", help="another build of libnc_gpuhash.so (same-box A/B of builds)")
@@ -69,12 +74,16 @@ def main():
                 for tag in args.tags.split(","):
                     tg = None if tag == "none" else tag.encode()
 
-                    def launch():
+                    def launch_sidx():
                         t.server_idx_device(mode, dist, keys, off, conts[dist], 8, hash_tag=tg, out=out,
                                             shape=shape, key_end=kb)
+
+                    def launch_hash():
+                        t.hash_batch_device(mode, keys, off, out, shape=shape, key_end=kb)
                     ref, res = None, {}
                     for name, v in PIPES.items():
-                        L.lib().nc_gpuhash_set_tuning(GRIDS.get(name, 0), 0, v)
+                        launch = launch_hash if v is None else launch_sidx
+                        L.lib().nc_gpuhash_set_tuning(GRIDS.get(name, 0), 0, v or 0)
                         out.fill_(-1)
                         launch()
                         torch.cuda.synchronize()
@@ -86,6 +95,11 @@ def main():
                             d = np.flatnonzero(h != ref)
                             chk = "same" if d.size == 0 else f"DIFF {d.size} first {int(d[0])}"
                         ms = []
+                        t_end = time.perf_counter() + args.spinup
+                        while time.perf_counter() < t_end:
+                            for _ in range(10):
+                                launch()
+                            torch.cuda.synchronize()
                         for _ in range(args.rounds):
                             for _ in range(3):
                                 launch()

@@ -252,39 +252,53 @@ __device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const 
     return idx[lo == n ? 0u : lo];
 }
 
-/* The same over a PACKED LDS continuum, one word per point: the value's top
- * 24 bits over the server index (w = v & ~255 | server, pools of <= 256
- * servers), followed by four 0xffffffff sentinels (never below a hash's top
- * 24 bits, so a scan stops at them without bounds checks). 4 bytes a point
- * keep a 1280-point pool inside the grouped pipeline's four workgroups per
- * CU. A 512-entry u16 bucket index over the hash's top 9 bits (~2.5 points a
- * bucket) starts a SCAN four points at a time (two ds_read2_b32): most keys
- * resolve in two LDS round trips. The scan compares h >> 8; only when the
- * found point shares h's top 24 bits is the answer ambiguous, and that lane
+/* ketama_dispatch over a PACKED LDS continuum, one word per point: the
+ * value's top 24 bits over the server index (w = v & ~255 | server, pools of
+ * <= 256 servers), followed by eight sentinels 0xffffff00 | point 0's server
+ * (never below a hash's top 24 bits, so a search stops at them without bounds
+ * checks, and a lane that stops on one reads the wrap's answer from it). 4
+ * bytes a point keep a 1280-point pool inside the grouped pipeline's four
+ * workgroups per CU. A 512-entry u16 bucket index over the hash's top 9 bits
+ * (~2.5 points a bucket) gives the start; from it rounded down to a multiple
+ * of four, EIGHT words (two ds_read_b128) are searched by three compares on
+ * the sorted words (quad, pair, word) for the first word >= hb = h & ~255
+ * (the words before the bucket start are below hb: they are below the
+ * bucket's first value). A lane needs a second round only when eight points
+ * of its bucket lie below h (P ~ 0.002), so a wave of 64 lanes almost always
+ * resolves in two LDS round trips (the four-word scan of rounds 3-4 ran two
+ * rounds in most waves: C2 0.509-0.512 -> 0.474-0.476 ms,
+ * profiles/r05_sidx_s8_ab.jsonl). Only when the found word shares h's top 24
+ * bits is the answer ambiguous (about one key in 13000 for 1280 points, or h
+ * >= 0xffffff00 against a sentinel): that lane finds the word's index and
  * walks the run of such points comparing full values from the continuum in
- * global memory (cont: {server, value} pairs) — about one key in 13000 for
- * 1280 points. Past the last point the answer wraps to point 0 (w0). */
-__device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, const uint16_t *bkt16,
-                                                           const uint32_t *cont, uint32_t n, uint32_t w0, uint32_t h)
+ * global memory (cont: {server, value} pairs); past the last point the answer
+ * wraps to point 0 (w0). */
+__device__ __forceinline__ uint32_t ketama_find_lds_packed8(const uint32_t *w, const uint16_t *bkt16,
+                                                            const uint32_t *cont, uint32_t n, uint32_t w0, uint32_t h)
 {
+    using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
     const uint32_t hb = h & ~0xffu; /* w >> 8 < h >> 8  <=>  w < hb */
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(__builtin_assume_aligned(w, 16));
+    /* the first of the eight sorted words >= hb; the last one if none is */
+    auto first_ge = [&](const u32x4 &a, const u32x4 &b) __attribute__((always_inline)) {
+        const u32x4 d = a.w < hb ? b : a;
+        const bool p2 = d.y < hb;
+        const uint32_t e0 = p2 ? d.z : d.x, e1 = p2 ? d.w : d.y;
+        return e0 < hb ? e1 : e0;
+    };
     /* clamped: an unsorted continuum (a caller error) could leave a bucket
-     * unwritten; from at most n the scan still ends at the sentinels */
-    uint32_t lo = min((uint32_t)bkt16[h >> 23], n);
-    uint32_t pos, cand;
-    for (;;) {
-        const uint32_t c0 = w[lo], c1 = w[lo + 1u], c2 = w[lo + 2u], c3 = w[lo + 3u];
-        /* sorted words: those below h come first */
-        const uint32_t k = (uint32_t)(c0 < hb) + (uint32_t)(c1 < hb) + (uint32_t)(c2 < hb) + (uint32_t)(c3 < hb);
-        if (k < 4u) {
-            pos = lo + k;
-            cand = k == 0u ? c0 : (k == 1u ? c1 : (k == 2u ? c2 : c3));
-            break;
-        }
-        lo += 4u; /* all four below h */
+     * unwritten; from at most n the search still ends at the sentinels (it
+     * goes on only while the eighth word is below hb, so it never reads past
+     * word n + 7) */
+    uint32_t lo = min((uint32_t)bkt16[h >> 23], n) & ~3u;
+    uint32_t cand = first_ge(q[lo >> 2], q[(lo >> 2) + 1u]);
+    while (cand < hb) { /* rare: all eight below h */
+        lo += 8u;
+        cand = first_ge(q[lo >> 2], q[(lo >> 2) + 1u]);
     }
-    if (pos >= n) return w0 & 0xffu; /* past the last point: the wrap */
     if ((cand ^ hb) < 0x100u) { /* rare, the same top 24 bits: full values decide */
+        uint32_t pos = lo;
+        while (w[pos] < hb) pos++;
         while (pos < n && (w[pos] ^ hb) < 0x100u && cont[2u * pos + 1u] < h) pos++;
         cand = pos < n ? w[pos] : w0;
     }
@@ -961,10 +975,13 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
             if (i == n - 1u)
                 for (uint32_t bb = cb + 1u; bb < 256u; bb++) tab[bb] = n;
         }
-    } else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked) {
+    } else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked && (VAR & 512) == 0) { /* bit 9: DIAGNOSTIC */
         pw0 = (dist.cont[1] & ~0xffu) | (dist.cont[0] & 0xffu); /* point 0, the wrap's answer */
-        for (uint32_t i = t; i < dist.ncont + 4u; i += TK) /* + four sentinels */
-            gs_cont[i] = i < dist.ncont ? (dist.cont[2u * i + 1u] & ~0xffu) | (dist.cont[2u * i] & 0xffu) : ~0u;
+        /* + eight sentinels: never below a hash's top 24 bits, point 0's
+         * server in the low byte (ketama_find_lds_packed8) */
+        for (uint32_t i = t; i < dist.ncont + 8u; i += TK)
+            gs_cont[i] = i < dist.ncont ? (dist.cont[2u * i + 1u] & ~0xffu) | (dist.cont[2u * i] & 0xffu)
+                                        : 0xffffff00u | (pw0 & 0xffu);
         /* the u16[512] bucket starts (in the table's 1 KiB) from the staged
          * words, not by 512 binary searches over global memory (eleven
          * dependent L2 round trips in every workgroup's prologue): point i
@@ -1090,8 +1107,8 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
                 h = ketama_find_lds(gs_cont, reinterpret_cast<const uint8_t *>(gs_cont + dist.ncont), tab, dist.ncont,
                                     h);
             else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked && (VAR & 128) == 0) /* bit 7: DIAGNOSTIC */
-                h = ketama_find_lds_packed(gs_cont, reinterpret_cast<const uint16_t *>(tab), dist.cont, dist.ncont,
-                                           pw0, h);
+                h = ketama_find_lds_packed8(gs_cont, reinterpret_cast<const uint16_t *>(tab), dist.cont, dist.ncont,
+                                            pw0, h);
 
             if constexpr (CS) {
                 gs_ds_write_b32(lds_base + G::kRes + (it & 1u) * 4u * TK + 4u * i, h);
@@ -1931,7 +1948,7 @@ constexpr int kVarGsortCs = 1 << 27; /* its hashes stored once per tile, 16 byte
 constexpr int kVarGsort512 = 1 << 26; /* with kVarGsortCs: 512-key tiles, eight waves (length octiles) */
 constexpr int kVarGsortIssue = 1 << 28; /* A/B: the grouped tile's DMAs issued before the previous tile's store */
 constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline stages in LDS (5 B each) */
-constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 4 sentinels), beside four 512-key
+constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 8 sentinels), beside four 512-key
                                             workgroups per CU */
 constexpr int kVarNoPacked = 1 << 27; /* server_idx A/B: the 5-byte LDS continuum even where the packed one fits */
 /* direct byte kernels' options beyond bits 20-23, in bits only the ring
@@ -2124,6 +2141,9 @@ hipError_t launch_gs_mode(const uint8_t *base, const uint64_t *off, uint64_t del
         if ((var & kVarGsortIssue) != 0 && (var & kVarGsort512) != 0) /* A/B: DMAs before the store */
             return launch_gs<MODE, 64, 2, true, 512>(base, off, delta, nkeys, out, stream, var);
         if constexpr (MODE == NC_GPUHASH_FNV1A_64) { /* DIAGNOSTIC A/B (bits 29-30): occupancy vs slab size */
+            if ((var & kVarGsort512) != 0 && (var & (3 << 29)) == (3 << 29)) /* both: the 5 KiB as dynamic LDS */
+                return launch_gs<MODE, 0, 2, true, 512, 5136>(base, off, delta, nkeys, out, stream, var,
+                                                              WrDist{nullptr, 0u, 0u, nullptr}, 5136);
             if ((var & kVarGsort512) != 0 && (var & (1 << 29)) != 0) /* 6400 B of unused dynamic LDS */
                 return launch_gs<MODE, 0, 2, true, 512>(base, off, delta, nkeys, out, stream, var,
                                                         WrDist{nullptr, 0u, 0u, nullptr}, 6400);
@@ -2339,8 +2359,8 @@ hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t 
                      * tiles' budget: four workgroups per CU, as without a
                      * dispatch */
                     const int sets = (d.gs_var & (3 << 21)) != 0 ? d.gs_var : (d.gs_var | (2 << 21));
-                    constexpr int kR = (kLdsPackedMax + 4) * 4;
-                    const size_t dyn = ((size_t)d.ncont + 4u) * 4u;
+                    constexpr int kR = (kLdsPackedMax + 8) * 4;
+                    const size_t dyn = ((size_t)d.ncont + 8u) * 4u;
                     if constexpr (MODE == NC_GPUHASH_FNV1A_64) { /* DIAGNOSTIC (tuning bits 19 / 20): what the
                                                                     dispatch costs — no hash_tag code / no search */
                         switch ((d.gs_var >> 19) & 3) {
@@ -2348,7 +2368,11 @@ hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t 
                                                                                             stream, sets, wd, dyn);
                         case 2: return launch_gs<MODE, (5 << 12) | 128, 2, true, 512, kR>(base, off, delta, nkeys, out,
                                                                                             stream, sets, wd, dyn);
-                        case 3: return launch_gs<MODE, (5 << 12) | 384, 2, true, 512, kR>(base, off, delta, nkeys, out,
+                        case 3:
+                            if (d.gs_var & (1 << 26)) /* ... and no continuum staging in the prologue */
+                                return launch_gs<MODE, (5 << 12) | 896, 2, true, 512, kR>(base, off, delta, nkeys, out,
+                                                                                            stream, sets, wd, dyn);
+                            return launch_gs<MODE, (5 << 12) | 384, 2, true, 512, kR>(base, off, delta, nkeys, out,
                                                                                             stream, sets, wd, dyn);
                         default: break;
                         }
