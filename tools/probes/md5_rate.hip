@@ -9,6 +9,9 @@
 //   form 4: T in 64 SGPRs set before the loop, v_add3(a, w, sT), +f (VOP2)
 //   form 5: form 2's ops, the 61 steps as one inline-asm statement
 //           (md5_asm.inc, tools/gen_md5_asm.py): no hazard s_nops
+//   form 6: form 0's ops as one inline-asm statement (w+T into two
+//           alternating scratch registers), step i+1's w+T after step i's
+//           v_add3; form 7: the same with each w+T first in its step
 // Prints a check of form 5 against form 0, then ns per 64-lane round per SIMD
 // and the implied C3 time (2^20 rounds over 1024 SIMDs). Built by
 // twemproxy_amd/csrc/Makefile (target all).
@@ -36,6 +39,19 @@ __device__ __forceinline__ void md5_steps_asm_0_61(uint32_t (&v)[4], const uint3
 {
     uint32_t t; /* scratch */
     asm(NC_MD5_ASM_STEPS_0_61 NC_MD5_ASM_OPERANDS(v, w, t));
+}
+
+#define NC_MD5_ASM6_OPERANDS(v, w, t, t5, t6)                                                               \
+    : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "=&v"(t), "=&v"(t5), "=&v"(t6)                      \
+    : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]), "v"(w[8]), \
+      "v"(w[9]), "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15])
+
+template <int FORM>
+__device__ __forceinline__ void md5_steps_asm67_0_61(uint32_t (&v)[4], const uint32_t (&w)[16])
+{
+    uint32_t t, t5, t6;
+    if constexpr (FORM == 6) asm(NC_MD5_ASM6_STEPS_0_61 NC_MD5_ASM6_OPERANDS(v, w, t, t5, t6));
+    else asm(NC_MD5_ASM7_STEPS_0_61 NC_MD5_ASM6_OPERANDS(v, w, t, t5, t6));
 }
 
 __device__ __forceinline__ void md5_steps_asm_61_64(uint32_t (&v)[4], const uint32_t (&w)[16])
@@ -100,6 +116,7 @@ __global__ __launch_bounds__(256) void md5_rounds(unsigned *out, int rounds)
     for (int r = 0; r < rounds; r++) {
         uint32_t v[4] = {0x67452301u + acc, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
         if constexpr (FORM == 5) md5_steps_asm_0_61(v, w);
+        else if constexpr (FORM >= 6) md5_steps_asm67_0_61<FORM>(v, w);
         else steps<FORM>(v, w, sT, std::make_integer_sequence<int, 61>{});
         acc += v[0];
         w[r & 15] ^= acc; /* keeps the rounds dependent on each other's data */
@@ -138,6 +155,9 @@ __global__ void md5_check(unsigned *out)
     if constexpr (FORM == 5) {
         md5_steps_asm_0_61(v, w);
         md5_steps_asm_61_64(v, w);
+    } else if constexpr (FORM >= 6) {
+        md5_steps_asm67_0_61<FORM>(v, w);
+        md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
     } else {
         md5_steps(v, w, std::make_integer_sequence<int, 61>{});
         md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
@@ -152,14 +172,23 @@ int main()
     unsigned *o;
     (void)hipMalloc(&o, 1 << 20);
     {
-        unsigned h0[256], h5[256];
+        unsigned h0[256], h5[256], h6[256], h7[256];
         hipLaunchKernelGGL(md5_check<0>, dim3(1), dim3(64), 0, 0, o);
         (void)hipMemcpy(h0, o, sizeof h0, hipMemcpyDeviceToHost);
         hipLaunchKernelGGL(md5_check<5>, dim3(1), dim3(64), 0, 0, o);
         (void)hipMemcpy(h5, o, sizeof h5, hipMemcpyDeviceToHost);
-        int bad = 0;
-        for (int i = 0; i < 256; i++) bad += h0[i] != h5[i];
-        printf("{\"asm_steps_match\": %s, \"mismatches\": %d}\n", bad ? "false" : "true", bad);
+        hipLaunchKernelGGL(md5_check<6>, dim3(1), dim3(64), 0, 0, o);
+        (void)hipMemcpy(h6, o, sizeof h6, hipMemcpyDeviceToHost);
+        hipLaunchKernelGGL(md5_check<7>, dim3(1), dim3(64), 0, 0, o);
+        (void)hipMemcpy(h7, o, sizeof h7, hipMemcpyDeviceToHost);
+        int bad = 0, bad6 = 0, bad7 = 0;
+        for (int i = 0; i < 256; i++) {
+            bad += h0[i] != h5[i];
+            bad6 += h0[i] != h6[i];
+            bad7 += h0[i] != h7[i];
+        }
+        printf("{\"asm_steps_match\": %s, \"mismatches\": %d, \"form6_mismatches\": %d, \"form7_mismatches\": %d}\n",
+               bad ? "false" : "true", bad, bad6, bad7);
     }
     for (int wps : {4, 8}) {
         run<0>(wps, o, p.multiProcessorCount);
@@ -168,6 +197,8 @@ int main()
         run<3>(wps, o, p.multiProcessorCount);
         run<4>(wps, o, p.multiProcessorCount);
         run<5>(wps, o, p.multiProcessorCount);
+        run<6>(wps, o, p.multiProcessorCount);
+        run<7>(wps, o, p.multiProcessorCount);
     }
     return 0;
 }
