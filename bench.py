@@ -180,7 +180,7 @@ def md5_ceiling():
         out = subprocess.run([exe], capture_output=True, text=True, timeout=60, check=True).stdout
     except Exception:
         return None
-    rows = [json.loads(l) for l in out.splitlines() if l.startswith("{") and "form" in l]
+    rows = [r for r in (json.loads(l) for l in out.splitlines() if l.startswith("{")) if "ns_per_round_per_simd" in r]
     best = min(rows, key=lambda r: r["ns_per_round_per_simd"], default=None)
     if best is None:
         return None
