@@ -260,44 +260,45 @@ __device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const 
  * bytes a point keep a 1280-point pool inside the grouped pipeline's four
  * workgroups per CU. A 512-entry u16 bucket index over the hash's top 9 bits
  * (~2.5 points a bucket) gives the start; from it rounded down to a multiple
- * of four, EIGHT words (two ds_read_b128) are searched by three compares on
- * the sorted words (quad, pair, word) for the first word >= hb = h & ~255
- * (the words before the bucket start are below hb: they are below the
- * bucket's first value). A lane needs a second round only when eight points
- * of its bucket lie below h (P ~ 0.002), so a wave of 64 lanes almost always
- * resolves in two LDS round trips (the four-word scan of rounds 3-4 ran two
- * rounds in most waves: C2 0.509-0.512 -> 0.474-0.476 ms,
- * profiles/r05_sidx_s8_ab.jsonl). Only when the found word shares h's top 24
- * bits is the answer ambiguous (about one key in 13000 for 1280 points, or h
- * >= 0xffffff00 against a sentinel): that lane finds the word's index and
- * walks the run of such points comparing full values from the continuum in
- * global memory (cont: {server, value} pairs); past the last point the answer
- * wraps to point 0 (w0). */
+ * of four, the aligned quad (one ds_read_b128) holds the first word >= hb =
+ * h & ~255 unless its last word is below hb, and then the next quads do (the
+ * words before the bucket start are below hb: they are below the bucket's
+ * first value). Within the quad two compares on the sorted words (pair, word)
+ * pick it. The search is bound by LDS bank conflicts, not by ALU: the
+ * four-word scan from the unaligned bucket start (rounds 3-4: two
+ * ds_read2_b32 a round, two rounds in most waves) cost C2 0.509-0.512 ms,
+ * eight words in two ds_read_b128 0.470-0.475, the quad first 0.467-0.468
+ * (profiles/r05_sidx_s8_ab.jsonl, r05_sidx_quad_ab.jsonl). Only when the
+ * found word shares h's top 24 bits is the answer ambiguous (about one key in
+ * 13000 for 1280 points, or h >= 0xffffff00 against a sentinel): that lane
+ * finds the word's index and walks the run of such points comparing full
+ * values from the continuum in global memory (cont: {server, value} pairs);
+ * past the last point the answer wraps to point 0 (w0). */
 __device__ __forceinline__ uint32_t ketama_find_lds_packed8(const uint32_t *w, const uint16_t *bkt16,
                                                             const uint32_t *cont, uint32_t n, uint32_t w0, uint32_t h)
 {
     using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
     const uint32_t hb = h & ~0xffu; /* w >> 8 < h >> 8  <=>  w < hb */
     const u32x4 *q = reinterpret_cast<const u32x4 *>(__builtin_assume_aligned(w, 16));
-    /* the first of the eight sorted words >= hb; the last one if none is */
-    auto first_ge = [&](const u32x4 &a, const u32x4 &b) __attribute__((always_inline)) {
-        const u32x4 d = a.w < hb ? b : a;
-        const bool p2 = d.y < hb;
-        const uint32_t e0 = p2 ? d.z : d.x, e1 = p2 ? d.w : d.y;
-        return e0 < hb ? e1 : e0;
-    };
     /* clamped: an unsorted continuum (a caller error) could leave a bucket
      * unwritten; from at most n the search still ends at the sentinels (it
-     * goes on only while the eighth word is below hb, so it never reads past
-     * word n + 7) */
+     * goes on only while a quad's last word is below hb, so it never reads
+     * past word n + 3) */
     uint32_t lo = min((uint32_t)bkt16[h >> 23], n) & ~3u;
-    uint32_t cand = first_ge(q[lo >> 2], q[(lo >> 2) + 1u]);
-    while (cand < hb) { /* rare: all eight below h */
-        lo += 8u;
-        cand = first_ge(q[lo >> 2], q[(lo >> 2) + 1u]);
+    u32x4 a = q[lo >> 2];
+    if (a.w < hb) { /* the quad's four words all below h: the next ones */
+        do {
+            lo += 4u;
+            a = q[lo >> 2];
+        } while (a.w < hb);
     }
+    const bool p2 = a.y < hb;
+    const uint32_t e0 = p2 ? a.z : a.x, e1 = p2 ? a.w : a.y;
+    uint32_t cand = e0 < hb ? e1 : e0;
     if ((cand ^ hb) < 0x100u) { /* rare, the same top 24 bits: full values decide */
-        uint32_t pos = lo;
+        /* from the bucket start again (re-read: keeping lo live past the
+         * search loop makes hipcc carry derived addresses through it) */
+        uint32_t pos = min((uint32_t)bkt16[h >> 23], n) & ~3u;
         while (w[pos] < hb) pos++;
         while (pos < n && (w[pos] ^ hb) < 0x100u && cont[2u * pos + 1u] < h) pos++;
         cand = pos < n ? w[pos] : w0;
