@@ -274,8 +274,8 @@ __device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const 
  * finds the word's index and walks the run of such points comparing full
  * values from the continuum in global memory (cont: {server, value} pairs);
  * past the last point the answer wraps to point 0 (w0). */
-__device__ __forceinline__ uint32_t ketama_find_lds_packed8(const uint32_t *w, const uint16_t *bkt16,
-                                                            const uint32_t *cont, uint32_t n, uint32_t w0, uint32_t h)
+__device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, const uint16_t *bkt16,
+                                                           const uint32_t *cont, uint32_t n, uint32_t w0, uint32_t h)
 {
     using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
     const uint32_t hb = h & ~0xffu; /* w >> 8 < h >> 8  <=>  w < hb */
@@ -979,7 +979,7 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
     } else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked && (VAR & 512) == 0) { /* bit 9: DIAGNOSTIC */
         pw0 = (dist.cont[1] & ~0xffu) | (dist.cont[0] & 0xffu); /* point 0, the wrap's answer */
         /* + eight sentinels: never below a hash's top 24 bits, point 0's
-         * server in the low byte (ketama_find_lds_packed8) */
+         * server in the low byte (ketama_find_lds_packed) */
         for (uint32_t i = t; i < dist.ncont + 8u; i += TK)
             gs_cont[i] = i < dist.ncont ? (dist.cont[2u * i + 1u] & ~0xffu) | (dist.cont[2u * i] & 0xffu)
                                         : 0xffffff00u | (pw0 & 0xffu);
@@ -1108,8 +1108,8 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
                 h = ketama_find_lds(gs_cont, reinterpret_cast<const uint8_t *>(gs_cont + dist.ncont), tab, dist.ncont,
                                     h);
             else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked && (VAR & 128) == 0) /* bit 7: DIAGNOSTIC */
-                h = ketama_find_lds_packed8(gs_cont, reinterpret_cast<const uint16_t *>(tab), dist.cont, dist.ncont,
-                                            pw0, h);
+                h = ketama_find_lds_packed(gs_cont, reinterpret_cast<const uint16_t *>(tab), dist.cont, dist.ncont,
+                                           pw0, h);
 
             if constexpr (CS) {
                 gs_ds_write_b32(lds_base + G::kRes + (it & 1u) * 4u * TK + 4u * i, h);
