@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--spinup", type=float, default=0.5, help="seconds of untimed launches before each entry "
                     "(device clocks ramp up under load, as bench.py's SPINUP_S)")
     ap.add_argument("--grids", default="", help="comma-separated grid caps for extra workgroup entries")
+    ap.add_argument("--gs-grids", default="", help="comma-separated grid caps for extra grouped-pipeline entries")
     ap.add_argument("--pipes", default="", help="comma-separated subset of the pipeline names")
     ap.add_argument("--lib", default="", help="another build of libnc_gpuhash.so (same-box A/B of builds)")
     args = ap.parse_args()
@@ -49,6 +50,9 @@ def main():
     for g in filter(None, args.grids.split(",")):
         PIPES[f"workgroup_g{g}"] = 1 << 29
         GRIDS[f"workgroup_g{g}"] = int(g)
+    for g in filter(None, args.gs_grids.split(",")):  # the grouped pipeline (packed continuum) at a grid cap
+        PIPES[f"grouped_g{g}"] = 1 << 30
+        GRIDS[f"grouped_g{g}"] = int(g)
 
     import numpy as np
     import torch
