@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X batched key hasher (BASELINE.json metric).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]   (N > 1: starts N rank processes itself)
     torchrun --nproc-per-node N ... bench.py --gpus N ...   (one rank per GPU, RCCL)
 
 Headline (BASELINE.json configs[1]): fnv1a_64 over 2^26
@@ -11,7 +11,8 @@ rank 0 generates all N x 2^26 keys and scatters byte-balanced ranges over
 RCCL (grouped point-to-point); scatter time is reported separately and is
 not part of `value` (weak scaling: fixed keys per GPU).
 
-Rank 0 prints ONE JSON line. `value` = total keys hashed by all ranks per
+Rank 0 prints ONE JSON line (a summary under ~5 KB; the full record goes to
+--detail-out). `value` = total keys hashed by all ranks per
 second (Mkeys/s) over K timed steps, max over ranks. Beside it, each timed
 with HIP events on the launch stream:
   md5         the same C2 keys (the metric's second mode), against the VALU
@@ -69,7 +70,110 @@ def parse():
                    help="process-group backend for N > 1 (nccl = RCCL; gloo stages the scatter through host memory)")
     p.add_argument("--same-device", action="store_true",
                    help="every rank on cuda:0: the one-GPU rehearsal of the N > 1 code (tests/test_gpu_bench_dist.py)")
+    p.add_argument("--launch-check", action="store_true",
+                   help="start the ranks, rendezvous over gloo and report them; no device work (tests/test_launch.py)")
+    p.add_argument("--detail-out", default=None,
+                   help="where rank 0 writes the full record (default gpurun_out/bench_detail.json when that "
+                        "directory exists); the printed line is its summary")
     return p.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_devices() -> int:
+    """GPUs this process may use. torch.cuda.device_count() does not
+    initialise the GPU on this image, so the launching parent may call it."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def spawn_ranks(args) -> int | None:
+    """`python3 bench.py --gpus N` with no launcher around it: start N fresh
+    rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one per
+    GPU) before this process touches any GPU, pass their output through, and
+    return the worst child exit code. Returns None when this process is
+    itself the rank to run (N = 1, or a launcher such as torch.distributed.run
+    already set WORLD_SIZE — which must then equal --gpus)."""
+    import signal
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            log(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+            return 2
+        return None
+    if args.gpus < 1:
+        log(f"bench.py: --gpus {args.gpus} < 1")
+        return 2
+    if not args.same_device:
+        ndev = visible_devices()
+        if args.gpus > ndev:
+            log(f"bench.py: --gpus {args.gpus} but {ndev} GPU(s) are visible")
+            return 2
+    if args.gpus == 1:
+        return None
+    port = str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]], env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+
+    signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    # a rank that fails leaves its peers blocked in a collective: give them a
+    # grace period, then stop them (their exact PIDs, never a pattern)
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
+            failed_at = time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > float(os.environ.get("NC_BENCH_GRACE_S", 30)):
+            stop()
+            for p in procs:
+                try:
+                    p.wait(10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.1)
+    for p in procs:
+        p.wait()
+    # the first rank to fail names the job's failure (the ranks stopped after
+    # it exit by SIGTERM)
+    first = next((p.returncode for p in sorted(procs, key=lambda p: p.returncode in (-15, 143))
+                  if p.returncode != 0), 0)
+    return first if first >= 0 else 128 - first
+
+
+def launch_check(args, world: int, rank: int, local: int) -> None:
+    """--launch-check: the rendezvous the bench's ranks make, on gloo, with
+    no device work; rank 0 prints every rank's view of the job."""
+    import torch.distributed as dist
+
+    if os.environ.get("NC_BENCH_FAIL_RANK") == str(rank):  # tests/test_launch.py: a rank that dies early
+        sys.exit(3)
+    me = {"rank": rank, "local_rank": local, "world": world, "pid": os.getpid()}
+    views = [me]
+    if world > 1:
+        dist.init_process_group("gloo")
+        views = [None] * world
+        dist.all_gather_object(views, me)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "gpus_arg": args.gpus, "ranks": views}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def timed_steps(t, torch, mode, keys, off, out, steps, warmup, dist_on, shape=None, launch=None, key_end=None):
@@ -360,14 +464,23 @@ def leg(t, torch, mode, keys, off, out, steps, warmup, dist_on, shape, key_end, 
 
 def main():
     args = parse()
+    rc = spawn_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:
+        local = 0
+    if args.launch_check:
+        return launch_check(args, world, rank, local)
     import torch
 
     global COMM_DEV
-    if args.same_device:
-        local = 0
+    ndev = torch.cuda.device_count()
+    if local >= ndev or (not args.same_device and world > ndev):
+        log(f"bench.py: rank {rank} needs cuda:{local} of {world} ranks but {ndev} GPU(s) are visible")
+        sys.exit(2)
     torch.cuda.set_device(local)
     dist_on = world > 1
     if dist_on:
@@ -585,12 +698,116 @@ def main():
         except Exception as e:  # reported, never substituted for the GPU number
             res["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        path = args.detail_out
+        if path is None and os.path.isdir(os.path.join(HERE, "gpurun_out")):
+            path = os.path.join(HERE, "gpurun_out", "bench_detail.json")
+        line = summarize(res, os.path.relpath(path, HERE) if path else None)
+        if path:
+            with open(path, "w") as f:
+                json.dump(res, f, indent=1)
+        print(json.dumps(line, separators=(",", ":")), flush=True)
     if dist_on:
         import torch.distributed as dist
 
         dist.barrier()
         dist.destroy_process_group()
+
+
+NORTH_STAR_FRAC = 0.70  # BASELINE.json north_star: >= 70 % of HBM peak on C3 fnv1a_64
+
+
+def _rf(r: dict | None, keep=("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_over_alg")) -> dict | None:
+    if r is None:
+        return None
+    return {k: r[k] for k in keep if k in r}
+
+
+def _leg(x: dict | None, extra=()) -> dict | None:
+    """one leg of the full record, cut to what a reader of the line needs"""
+    if x is None:
+        return None
+    if "error" in x:
+        return {"error": x["error"][:200]}
+    s = {k: x[k] for k in ("kernel_ms", "value", "unit") if k in x}
+    if "roofline" in x:
+        s["roofline"] = _rf(x["roofline"])
+    for k in extra:
+        if k in x:
+            s[k] = _rf(x[k], ("bound", "frac", "traffic_over_alg", "frac_of_md5_compute_ceiling"))
+    return s
+
+
+def summarize(res: dict, detail_path: str | None) -> dict:
+    """The printed line: the driver's contract fields, the headline roofline
+    and cpu_baseline, then every leg cut to kernel time, value and roofline
+    fraction (the whole record, per-depth C5 rows and ceilings included, goes
+    to `detail_path`). The driver keeps the last ~8 KB of stdout, so the line
+    must stay well under that; the north-star figure and the C2 md5 leg come
+    right after the headline."""
+    line = {k: res[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                                "gb_per_s_hashed", "kernel_ms_rank0", "kernel_ms_max", "variant", "roofline")
+            if k in res}
+    c3 = res.get("c3_fnv1a_64")
+    if c3 and "roofline" in c3:
+        rf = c3["roofline"]
+        line["north_star"] = {"workload": "C3 fnv1a_64 (BASELINE configs[2])", "kernel_ms": c3["kernel_ms"],
+                              "frac": rf["frac"], "target_frac": NORTH_STAR_FRAC,
+                              "met": rf["frac"] >= NORTH_STAR_FRAC, "traffic": rf.get("traffic"),
+                              "traffic_over_alg": rf.get("traffic_over_alg")}
+    if "md5" in res:
+        line["md5"] = _leg(res["md5"], ("roofline_hbm",))
+        if "roofline" in res["md5"]:
+            line["md5"]["roofline"] = _rf(res["md5"]["roofline"], ("bound", "achieved", "peak", "unit", "frac",
+                                                                    "frac_of_md5_compute_ceiling"))
+    if "server_idx_ketama" in res:
+        s = _leg(res["server_idx_ketama"])
+        if "kernel_ms" in s and res.get("kernel_ms_rank0"):
+            s["over_hash"] = round(s["kernel_ms"] / res["kernel_ms_rank0"] - 1.0, 4)
+        line["server_idx_ketama"] = s
+    for k in ("c3_fnv1a_64", "c3_crc32", "c3_md5"):
+        if k in res:
+            line[k] = _leg(res[k], ("roofline_lds", "roofline_hbm"))
+    if "c4_shard" in res:
+        c4 = res["c4_shard"]
+        line["c4_shard"] = {m: _leg(c4[m], ("roofline_valu",)) for m in ("md5", "crc32", "fnv1a_64") if m in c4}
+        if "scatter" in c4:
+            line["c4_shard"]["scatter"] = c4["scatter"]
+    for k in ("scatter", "c3_scatter"):
+        if k in res:
+            line[k] = res[k]
+    r = res.get("redis_key_extraction")
+    if r:
+        line["redis_key_extraction"] = r if "error" in r else {k: r[k] for k in ("ms_per_parse_wall", "mreq_s")}
+    for k in ("e2e_c2", "c4_ingest"):
+        e = res.get(k)
+        if e:
+            line[k] = {kk: e[kk] for kk in ("ms", "value", "unit", "h2d_gbs", "frac_of_h2d_probe", "parity", "error")
+                       if kk in e}
+    c5 = res.get("c5_e2e")
+    if c5:
+        if "error" in c5:
+            line["c5_e2e"] = c5
+        else:
+            def pt(r_):
+                return None if r_ is None else {k: r_[k] for k in ("path", "depth", "lanes", "submit_to_done_us",
+                                                                   "us_per_batch", "mkeys_s") if k in r_}
+            ring1 = next((r_ for r_ in c5["gpu"] if r_["path"].startswith("ring") and r_["depth"] == 1), None)
+            line["c5_e2e"] = {"host_per_key": pt(c5["host_per_key"]), "ring_depth1": pt(ring1),
+                              "ring_best_depth_ge2_le20us": pt(c5["ring_best_depth_ge2_le20us"]),
+                              "points": len(c5["gpu"]), "mismatches": c5["mismatches"]}
+    if "cpu_baseline" in res:
+        cb = res["cpu_baseline"]
+        line["cpu_baseline"] = cb if "error" in cb else {
+            **{k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "threads_share", "cpu_model")},
+            "mkeys_s_1thread": cb["detail"]["fnv1a_64"].get("mkeys_s_1threads"),
+            "md5_mkeys_s_all_cores": cb["detail"].get("md5", {}).get(f"mkeys_s_{cb['cores']}threads")}
+    par = res["parity"]
+    line["parity"] = {"all": par["all"], "legs": len(par["per_rank"]),
+                      "ranks": max((len(v) for v in par["per_rank"].values()), default=0),
+                      "bad": sorted(k for k, v in par["per_rank"].items() if any(x != "ok" for x in v))}
+    line["detail"] = detail_path
+    return line
 
 
 def h2d_probe(torch, src, dev, reps=3):

@@ -23,6 +23,7 @@ def line():
     assert p.returncode == 0, p.stderr[-3000:]
     rows = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(rows) == 1, p.stdout[-2000:]
+    assert len(rows[0]) < 6000  # the driver keeps ~8 KB of stdout: the whole line must survive
     return json.loads(rows[0])
 
 
@@ -69,3 +70,12 @@ def test_secondary_legs(line):
     for mode in ("md5", "crc32", "fnv1a_64"):
         assert line["c4_shard"][mode]["kernel_ms"] > 0
         assert line["c4_shard"][mode]["roofline"]["traffic"] is None
+
+
+def test_north_star_and_summary(line):
+    ns = line["north_star"]
+    assert ns["kernel_ms"] == line["c3_fnv1a_64"]["kernel_ms"] and ns["frac"] == line["c3_fnv1a_64"]["roofline"]["frac"]
+    assert ns["target_frac"] == 0.70 and ns["met"] == (ns["frac"] >= 0.70)
+    # the line is a summary: per-depth C5 rows live in the detail file only
+    assert "gpu" not in line["c5_e2e"] and line["c5_e2e"]["mismatches"] == 0
+    assert line["parity"]["all"] == "ok" and line["parity"]["bad"] == []

@@ -1,5 +1,6 @@
-"""bench.py's multi-rank code on the one-GPU box: `torch.distributed.run`
-starts bench.py as 2 ranks (``--backend gloo --same-device``: both ranks on
+"""bench.py's multi-rank code on the one-GPU box: bench.py starts itself as
+2 ranks (`python3 bench.py --gpus 2`, no launcher: spawn_ranks), and
+`torch.distributed.run` starts it as 2 ranks (the driver's form) (``--backend gloo --same-device``: both ranks on
 cuda:0, the scatter staged through host memory) at reduced sizes. Every
 N > 1 branch of bench.py runs — the process group, rank 0's generation and
 the root scatter of C2/C3/C4 (resident()), the max/sum over ranks, the
@@ -30,14 +31,18 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.fixture(scope="module")
-def line():
+@pytest.fixture(scope="module", params=["self", "torchrun"])
+def run(request, tmp_path_factory):
     import torch  # noqa: F401  (pages the image in before the children's own imports)
 
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={WORLD}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+    detail = str(tmp_path_factory.mktemp("bench") / "detail.json")
+    launcher = [] if request.param == "self" else [
+        "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={WORLD}",
+        "--master-addr", "127.0.0.1", "--master-port", str(_free_port())]
+    cmd = [sys.executable, *launcher,
            os.path.join(HERE, "bench.py"), "--gpus", str(WORLD), "--steps", "3", "--warmup", "1",
-           "--nkeys", str(NKEYS), "--c4-nkeys", str(C4_NKEYS), "--backend", "gloo", "--same-device"]
+           "--nkeys", str(NKEYS), "--c4-nkeys", str(C4_NKEYS), "--backend", "gloo", "--same-device",
+           "--detail-out", detail]
     # 64 KiB scatter messages: the C4 shard's 1 MiB goes in 16 rounds, as
     # an 8 GiB shard does in 1 GiB pieces on the 8-GPU node
     env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"),
@@ -46,7 +51,12 @@ def line():
     assert p.returncode == 0, p.stderr[-4000:]
     rows = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(rows) == 1, p.stdout[-2000:]  # rank 0 alone prints
-    return json.loads(rows[0])
+    return json.loads(rows[0]), json.load(open(detail))
+
+
+@pytest.fixture(scope="module")
+def line(run):
+    return run[0]
 
 
 def test_driver_fields_at_n2(line):
@@ -58,8 +68,10 @@ def test_driver_fields_at_n2(line):
     assert "cpu_baseline" not in line and "c5_e2e" not in line and "e2e_c2" not in line  # rank 0 at N = 1 only
 
 
-def test_every_rank_parity_ok(line):
-    par = line["parity"]
+def test_every_rank_parity_ok(run):
+    line, full = run
+    assert line["parity"] == {"all": "ok", "legs": 8, "ranks": WORLD, "bad": []}, line["parity"]
+    par = full["parity"]
     assert par["all"] == "ok", par
     want = {"C2/fnv1a_64", "C2/md5", "C3/fnv1a_64", "C3/crc32", "C3/md5", "C4/md5", "C4/crc32", "C4/fnv1a_64"}
     assert set(par["per_rank"]) == want
