@@ -805,7 +805,7 @@ def summarize(res: dict, detail_path: str | None) -> dict:
     par = res["parity"]
     line["parity"] = {"all": par["all"], "legs": len(par["per_rank"]),
                       "ranks": max((len(v) for v in par["per_rank"].values()), default=0),
-                      "bad": sorted(k for k, v in par["per_rank"].items() if any(x != "ok" for x in v))}
+                      "bad": sorted(k for k, v in par["per_rank"].items() if any(x not in ("ok", "unpinned") for x in v))}
     line["detail"] = detail_path
     return line
 

@@ -310,8 +310,9 @@ rstatus_t nc_gpuhash_host_unregister(void *ptr);
  * (the mbufs may be recycled on return) and publishes it with one store; the
  * lane's worker hashes it and writes the hashes and a completion word back
  * to host memory; poll is one load. The launch starts on the first batch,
- * ends after 10 ms with no batch on any lane or after 2 s (checked before
- * every batch, under load too), and is relaunched by the next submit or
+ * ends after 10 ms with no batch on any lane or after 2 s (checked after
+ * every batch and honoured before the next one is taken, under load too),
+ * and is relaunched by the next submit or
  * poll: a batch published while the launch ends is served on a later poll,
  * so poll (or wait) every ticket. Up to nslots batches in flight; lanes may
  * finish out of order. A live launch holds nlanes workgroup slots (one lane's
@@ -338,9 +339,18 @@ void nc_gpuhash_ring_destroy(nc_gpuhash_ring_t *r);
 rstatus_t nc_gpuhash_ring_submit_spans(nc_gpuhash_ring_t *r, int mode, const struct nc_keyspan *spans,
                                        uint32_t nkeys, uint32_t *out, int *ticket);
 /* NC_OK once the batch's hashes are in its `out`, NC_EAGAIN before, and
- * NC_ERROR/EINVAL for a ticket this ring never issued */
+ * NC_ERROR/EINVAL for a ticket this ring never issued. Lifetime: the ring
+ * keeps `out` until the batch is delivered — by this poll, or by the submit
+ * that reuses its slot — so `out` must stay valid until then, or be released
+ * with nc_gpuhash_ring_forget first. */
 rstatus_t nc_gpuhash_ring_poll(nc_gpuhash_ring_t *r, int ticket);
 rstatus_t nc_gpuhash_ring_wait(nc_gpuhash_ring_t *r, int ticket);
+/* the ticket's owner is going away (a client connection closed and freed
+ * its msg, src/nc_message.c:372-396): the batch still runs, but its hashes
+ * are never copied into its `out`, which may be freed on return. NC_OK
+ * (also for a ticket already delivered), NC_ERROR/EINVAL for a ticket this
+ * ring never issued */
+rstatus_t nc_gpuhash_ring_forget(nc_gpuhash_ring_t *r, int ticket);
 /* launches so far (the first submit's, and relaunches after idle or 2 s) */
 uint64_t nc_gpuhash_ring_launches(const nc_gpuhash_ring_t *r);
 /* the ring's lane count */

@@ -78,4 +78,5 @@ def test_north_star_and_summary(line):
     assert ns["target_frac"] == 0.70 and ns["met"] == (ns["frac"] >= 0.70)
     # the line is a summary: per-depth C5 rows live in the detail file only
     assert "gpu" not in line["c5_e2e"] and line["c5_e2e"]["mismatches"] == 0
-    assert line["parity"]["all"] == "ok" and line["parity"]["bad"] == []
+    # 2^20 keys has no reference digest ("unpinned"); a mismatch would be named in "bad"
+    assert line["parity"]["all"] in ("ok", "unpinned") and line["parity"]["bad"] == []

@@ -321,3 +321,60 @@ def test_ring_c_rejects_inverted_and_null_spans(gpu, oracle):
         r.wait(tk2)
         assert tk2 == 0  # the refused submits took no ticket
         assert out2.tolist() == [t.hash_key("fnv1a_64", bytes(range(10))), t.hash_key("fnv1a_64", bytes(range(10, 40)))]
+
+
+def test_ring_life_limit_with_every_slot_in_flight(gpu, oracle):
+    """the 2 s life limit under pipelined load: every slot stays submitted
+    (more than one batch per lane in flight, so a lane always finds its next
+    batch published when it polls) for 2.6 s; the launch must still end and
+    be relaunched, with every result equal to the oracle's"""
+    import collections
+
+    rng = np.random.default_rng(64)
+    bufs = [batch(rng, 200, maxlen=40) for _ in range(8)]
+    wants = [want(oracle, 6, b, s) for b, s in bufs]
+    nslots = 16
+    with t.Ring(0, nslots=nslots, lanes=4) as r:
+        inflight = collections.deque()
+        t_end = time.perf_counter() + 2.6
+        i = checked = 0
+        while time.perf_counter() < t_end:
+            if len(inflight) == nslots:
+                tk, out, j = inflight.popleft()
+                r.wait(tk)
+                np.testing.assert_array_equal(out, wants[j])
+                checked += 1
+            buf, spans = bufs[i % 8]
+            tk, out = r.submit_spans("fnv1a_64", buf, spans)
+            inflight.append((tk, out, i % 8))
+            i += 1
+        while inflight:
+            tk, out, j = inflight.popleft()
+            r.wait(tk)
+            np.testing.assert_array_equal(out, wants[j])
+            checked += 1
+        assert r.launches >= 2, (r.launches, checked)
+        assert checked == i
+
+
+def test_ring_forget_drops_the_copy(gpu, oracle):
+    """a forgotten ticket's batch still runs, its slot is reused normally,
+    and its output array is never written (its owner freed it)"""
+    rng = np.random.default_rng(65)
+    with t.Ring(0, nslots=2) as r:
+        buf, spans = batch(rng, 50, maxlen=30)
+        r.debug_hold(True)
+        tk, out = r.submit_spans("fnv1a_64", buf, spans)
+        out[:] = 7
+        r.forget(tk)
+        r.debug_hold(False)
+        r.wait(tk)
+        assert (out == 7).all()
+        # the slots go on serving: three more batches reuse both slots
+        for _ in range(3):
+            b2, s2 = batch(rng, 40, maxlen=30)
+            tk2, o2 = r.submit_spans("murmur", b2, s2)
+            r.wait(tk2)
+            np.testing.assert_array_equal(o2, want(oracle, 10, b2, s2))
+        with pytest.raises(Exception):
+            r.forget(123456)  # never issued

@@ -40,9 +40,10 @@
  *   host poll: one load of that word; the hashes are copied to the caller.
  *
  * The launch always ends: on `stop`; and once any lane finds the whole ring
- * idle for kIdleTicks, or the launch older than kLifeTicks (checked before
- * every batch, under load too), it sets the launch's `closing` word and
- * every lane leaves. Leaving is race-free per lane: the worker publishes its
+ * idle for kIdleTicks, or the launch older than kLifeTicks (checked when
+ * idle and after every batch, and honoured before the next batch is taken,
+ * so under load too), it sets the launch's `closing` word and every lane
+ * leaves, serving at most one more batch. Leaving is race-free per lane: the worker publishes its
  * lane's `exiting`, fences, then looks at its next slot's descriptor again
  * (and serves it if published); the host publishes a descriptor, fences,
  * then looks at that lane's `exiting`. At least one of them sees the other,
@@ -168,24 +169,40 @@ struct Poll {
 /* thread 0: a poll's outcome. 1: stop (go = 0) or the batch is published (go
  * = 1, lo = the descriptor's low word) or, once leaving, nothing came (go =
  * 0); -1: the launch is ending and `exiting` was just published (poll once
- * more); 0: keep polling. The idle and life limits as in the file comment. */
-__device__ __forceinline__ int poll_check(const Poll &p, uint32_t tag, uint32_t epoch, uint64_t born, uint64_t &last,
-                                          bool &leaving, RingCtl *c, RingDev *dv, uint32_t &go, uint32_t &lo)
+ * more); 0: keep polling. The idle and life limits as in the file comment:
+ * `closing` (another lane ended the launch) and `expired` (this lane's last
+ * batch finished past kLifeTicks, tested after each batch, off the batch's
+ * critical path) are honoured BEFORE a published batch is taken, so a lane
+ * that always finds its next batch waiting still leaves. Once leaving, the
+ * lane serves at most the one batch its post-`exiting` re-read found; every
+ * later one is the relaunch's (its `processed` says where to start). */
+__device__ __forceinline__ int poll_check(const Poll &p, uint32_t tag, uint32_t epoch, bool expired, uint64_t &last,
+                                          bool &leaving, bool &last_taken, RingCtl *c, RingDev *dv, uint32_t &go,
+                                          uint32_t &lo)
 {
     if (p.stop != 0u) return 1;
-    if ((uint32_t)(p.d >> 32) == tag) { /* published: the shape came with it */
+    const bool pub = (uint32_t)(p.d >> 32) == tag; /* published: the shape came with it */
+    if (leaving) { /* the descriptor was re-read after `exiting`: serve what it found, once; else the host relaunches */
+        if (pub && !last_taken) {
+            go = 1;
+            lo = (uint32_t)p.d;
+            last_taken = true;
+        }
+        return 1;
+    }
+    bool close = expired || p.closing == epoch;
+    if (pub && !close) {
         go = 1;
         lo = (uint32_t)p.d;
         return 1;
     }
-    if (leaving) return 1; /* the descriptor was re-read after `exiting`: the host relaunches */
-    const uint64_t now = ticks();
-    bool close = p.closing == epoch;
-    if (!close && now - born > kLifeTicks) close = true;
-    if (!close && now - last > kIdleTicks) {
-        const uint64_t any = __hip_atomic_load(&dv->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        close = now > any && now - any > kIdleTicks;
-        if (!close) last = any;
+    if (!close && !pub) {
+        const uint64_t now = ticks();
+        if (now - last > kIdleTicks) {
+            const uint64_t any = __hip_atomic_load(&dv->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            close = now > any && now - any > kIdleTicks;
+            if (!close) last = any;
+        }
     }
     if (!close) return 0;
     __hip_atomic_store(&dv->closing, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -221,7 +238,9 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
     uint32_t s = (uint32_t)(seq0 % nslots), tag = ring_tag(seq0);
     const uint64_t born = ticks();
     uint64_t last = born;
-    bool leaving = false; /* thread 0: `exiting` published and fenced */
+    bool leaving = false;    /* thread 0: `exiting` published and fenced */
+    bool last_taken = false; /* thread 0: the one batch a leaving lane serves was taken */
+    bool expired = false;    /* thread 0: a batch finished past kLifeTicks */
     uint64_t t_found = 0, t_staged = 0, t_issued = 0; /* thread 0: the diagnostic timeline (tl) */
     for (;;) {
         if (t == 0u) {
@@ -233,7 +252,7 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
             for (;;) {
                 Poll p;
                 p.issue(c, desc + s, dv);
-                const int r = poll_check(p, tag, epoch, born, last, leaving, c, dv, go, lo);
+                const int r = poll_check(p, tag, epoch, expired, last, leaving, last_taken, c, dv, go, lo);
                 if (r > 0) break;
                 if (r == 0) __builtin_amdgcn_s_sleep(2);
             }
@@ -308,6 +327,7 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
             __hip_atomic_store(&done[s], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&c->processed, done_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             last = ticks();
+            expired = last - born > kLifeTicks;
             __hip_atomic_fetch_max(&dv->last, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (tl != nullptr) { /* released; visible with the next batch's release */
                 tl[8 * s + 4] = last;
@@ -517,7 +537,8 @@ static int ring_reap(nc_gpuhash_ring_t *r, uint32_t s)
 {
     if (r->slot_state[s] == SLOT_FREE) return 1;
     if (__atomic_load_n(&r->done[s], __ATOMIC_ACQUIRE) != ring_tag(r->slot_seq[s])) return 0;
-    memcpy(r->slot_out[s], r->outs + (size_t)s * r->max_keys, (size_t)r->slot_nkeys[s] * sizeof(uint32_t));
+    if (r->slot_out[s] != NULL) /* NULL: the ticket was forgotten (its owner is gone) */
+        memcpy(r->slot_out[s], r->outs + (size_t)s * r->max_keys, (size_t)r->slot_nkeys[s] * sizeof(uint32_t));
     r->slot_state[s] = SLOT_FREE;
     return 1;
 }
@@ -619,6 +640,29 @@ extern "C" rstatus_t nc_gpuhash_ring_poll(nc_gpuhash_ring_t *r, int ticket)
             }
         }
     } /* older: its slot was reused, which delivered it first (ring_reap) */
+    pthread_mutex_unlock(&r->lock);
+    return rc;
+}
+
+extern "C" rstatus_t nc_gpuhash_ring_forget(nc_gpuhash_ring_t *r, int ticket)
+{
+    if (r == NULL || ticket < 0) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    pthread_mutex_lock(&r->lock);
+    const uint64_t back = (r->seq - (uint64_t)ticket) & kTagMask;
+    rstatus_t rc = NC_OK;
+    if (back == 0 || back > r->seq - r->seq0) {
+        errno = EINVAL;
+        rc = NC_ERROR;
+    } else if (back <= r->nslots) {
+        const uint64_t seq = r->seq - back;
+        const uint32_t s = (uint32_t)(seq % r->nslots);
+        /* the batch still runs and its slot is reaped as usual; only the copy
+         * into the caller's `out` is dropped */
+        if (r->slot_seq[s] == seq && r->slot_state[s] == SLOT_RUNNING) r->slot_out[s] = NULL;
+    } /* older: already delivered */
     pthread_mutex_unlock(&r->lock);
     return rc;
 }

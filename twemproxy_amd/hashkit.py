@@ -616,6 +616,12 @@ class Ring:
         L.check(self._lib.nc_gpuhash_ring_wait(self._h, ticket), "nc_gpuhash_ring_wait")
         self._keep.pop(ticket, None)
 
+    def forget(self, ticket: int) -> None:
+        """nc_gpuhash_ring_forget: the batch runs on, its hashes are never
+        copied into the ticket's output array"""
+        L.check(self._lib.nc_gpuhash_ring_forget(self._h, ticket), "nc_gpuhash_ring_forget")
+        self._keep.pop(ticket, None)
+
 
 class Pipe:
     """nc_gpuhash_pipe: whole host batches from caller-pinned memory, chunked
