@@ -355,6 +355,10 @@ rstatus_t nc_gpuhash_ring_forget(nc_gpuhash_ring_t *r, int ticket);
 uint64_t nc_gpuhash_ring_launches(const nc_gpuhash_ring_t *r);
 /* the ring's lane count */
 uint32_t nc_gpuhash_ring_lanes(const nc_gpuhash_ring_t *r);
+/* the ring's per-batch limits and slot count, as created (any pointer may be
+ * NULL); NC_ERROR/EINVAL for a NULL ring */
+rstatus_t nc_gpuhash_ring_limits(const nc_gpuhash_ring_t *r, uint32_t *max_keys, uint64_t *max_key_bytes,
+                                 uint32_t *nslots);
 
 /* ---- 4. multi-GPU shard planning ----
  * Split keys [0, nkeys) into nshards contiguous ranges with about equal key

@@ -22,6 +22,12 @@
  * tests/test_gpu_batch_site.py checks both against the indices the pure
  * reference build's fragment loops produced (tests/golden/proto_ref.json
  * "fragments").
+ *
+ * bs_pipeline runs the pipelined single-key site: client connections of one
+ * pool whose request streams are read in mbuf-sized reads and parsed by the
+ * reference's own read loop (msg_recv_chain's parse / split / repair), every
+ * parsed request deferred into the connection's read batch, one ring batch
+ * per read, and the requests forwarded in parse order when it is done.
  */
 #include "ref_proto_driver.c"
 
@@ -30,13 +36,14 @@
 #include "../integration/nc_batch_site.h"
 
 /* Returns the number of keys (ref_idx / batch_idx filled), -1 for a parse or
- * set-up failure, -2 when the ring refused the batch (every slot busy), -3
- * when the ring never finished it, -4 for a ring error. *polls counts the
- * NC_EAGAIN polls before the batch was done. */
+ * set-up failure, -3 when the ring never finished it, -4 for a ring error.
+ * *polls counts the NC_EAGAIN polls before the batch was done; *batches the
+ * ring batches the request took and *host_keys its keys hashed per key
+ * (longer than a ring batch holds). */
 int bs_request(int redis, const uint8_t *buf, uint32_t len, int mode, int dist, const char *const *names,
                const uint32_t *name_lens, const uint32_t *weights, uint32_t nserver, const uint8_t *tag,
                uint32_t taglen, nc_gpuhash_ring_t *ring, uint32_t *ref_idx, uint32_t *batch_idx, uint32_t kcap,
-               uint32_t *polls)
+               uint32_t *polls, uint32_t *batches, uint32_t *host_keys)
 {
     struct server_pool pool;
     struct conn fake_client;
@@ -63,23 +70,21 @@ int bs_request(int redis, const uint8_t *buf, uint32_t len, int mode, int dist, 
     const uint32_t nk = array_n(req->keys);
     struct nc_keyspan *span = malloc((nk + 1) * sizeof(*span));
     uint32_t *hashes = malloc((nk + 1) * sizeof(*hashes));
+    struct msg_hashes h;
     *polls = 0;
     if (req->result == MSG_PARSE_OK && nk <= kcap && span != NULL && hashes != NULL) {
         for (uint32_t i = 0; i < nk; i++) {
             const struct keypos *kp = array_get(req->keys, i);
             ref_idx[i] = msg_backend_idx(req, kp->start, (uint32_t)(kp->end - kp->start));
         }
-        int ticket;
-        rstatus_t st = msg_backend_hashes_submit(req, ring, span, hashes, &ticket);
-        if (st == NC_EAGAIN) {
-            rc = -2;
-        } else if (st != NC_OK) {
+        rstatus_t st = msg_backend_hashes_submit(req, ring, &h, span, hashes);
+        if (st != NC_OK) {
             rc = -4;
         } else {
             struct timespec t0, t1;
             clock_gettime(CLOCK_MONOTONIC, &t0);
             for (;;) {
-                st = msg_backend_hashes_poll(req, ring, span, hashes, ticket);
+                st = msg_backend_hashes_poll(req, &h);
                 if (st != NC_EAGAIN) break;
                 (*polls)++;
                 clock_gettime(CLOCK_MONOTONIC, &t1);
@@ -87,8 +92,11 @@ int bs_request(int redis, const uint8_t *buf, uint32_t len, int mode, int dist, 
             }
             if (st == NC_OK) {
                 msg_backend_idx_batch(req, hashes, batch_idx);
+                *batches = h.batches;
+                *host_keys = h.host_keys;
                 rc = (int)nk;
             } else {
+                msg_backend_hashes_forget(req, &h);
                 rc = st == NC_EAGAIN ? -3 : -4;
             }
         }
@@ -98,4 +106,301 @@ int bs_request(int redis, const uint8_t *buf, uint32_t len, int mode, int dist, 
     msg_put(req);
     rp_pool_deinit(&pool);
     return rc;
+}
+
+/*
+ * The teardown rule (nc_batch_site.h, Lifetime): submit request `buf` on a
+ * held ring (nc_gpuhash_ring_debug_hold: the batches stay in flight), forget
+ * it as a closing client's msg teardown would, release the ring, then push
+ * `reuse` more requests through every slot so the forgotten batches are
+ * reaped. Returns 1 when the forgotten msg's hashes[] (poisoned before the
+ * submit, kept alive here only to look at it) was never written, 0 when it
+ * was, -1 on failure.
+ */
+int bs_forget_probe(int redis, const uint8_t *buf, uint32_t len, int mode, int dist, const char *const *names,
+                    const uint32_t *name_lens, const uint32_t *weights, uint32_t nserver, nc_gpuhash_ring_t *ring,
+                    uint32_t reuse)
+{
+    struct server_pool pool;
+    struct conn fake_client;
+    if (!rp_ready || len > mbuf_data_size()) return -1;
+    if (rp_pool_init(&pool, mode, dist, names, name_lens, weights, nserver, NULL, 0) != 0) return -1;
+    memset(&fake_client, 0, sizeof(fake_client));
+    fake_client.owner = &pool;
+    fake_client.redis = redis ? 1 : 0;
+    int rc = -1;
+    struct mbuf *m = mbuf_get();
+    struct msg *req = m ? msg_get(&fake_client, 1, redis ? 1 : 0) : NULL;
+    if (req == NULL) {
+        if (m) mbuf_put(m);
+        rp_pool_deinit(&pool);
+        return -1;
+    }
+    req->state = 0;
+    req->token = NULL;
+    mbuf_copy(m, buf, len);
+    STAILQ_INIT(&req->mhdr);
+    mbuf_insert(&req->mhdr, m);
+    req->pos = m->start;
+    req->parser(req);
+    const uint32_t nk = array_n(req->keys);
+    struct nc_keyspan *span = malloc((nk + 1) * sizeof(*span));
+    uint32_t *hashes = malloc((nk + 1) * sizeof(*hashes));
+    uint32_t *ref = malloc((nk + 1) * sizeof(*ref)), *got = malloc((nk + 1) * sizeof(*got));
+    struct msg_hashes h;
+    if (req->result == MSG_PARSE_OK && nk > 0 && span && hashes && ref && got) {
+        for (uint32_t i = 0; i < nk; i++) hashes[i] = 0xA5A5A5A5u;
+        nc_gpuhash_ring_debug_hold(ring, 1);
+        rstatus_t st = msg_backend_hashes_submit(req, ring, &h, span, hashes);
+        msg_backend_hashes_forget(req, &h);
+        nc_gpuhash_ring_debug_hold(ring, 0);
+        rc = st == NC_OK ? 1 : -1;
+        for (uint32_t j = 0; rc == 1 && j < reuse; j++) {
+            uint32_t polls, b, hk;
+            if (bs_request(redis, buf, len, mode, dist, names, name_lens, weights, nserver, NULL, 0, ring, ref, got,
+                           nk, &polls, &b, &hk) != (int)nk)
+                rc = -1;
+        }
+        for (uint32_t i = 0; rc == 1 && i < nk; i++)
+            if (hashes[i] != 0xA5A5A5A5u) rc = 0;
+    }
+    free(span);
+    free(hashes);
+    free(ref);
+    free(got);
+    msg_put(req);
+    rp_pool_deinit(&pool);
+    return rc;
+}
+
+/* ---- the pipelined single-key site ---- */
+
+struct bs_conn {
+    struct conn c;           /* the client connection (owner of its msgs) */
+    const uint8_t *stream;   /* what the client sends */
+    uint32_t len, off;       /* bytes, bytes already read */
+    struct msg *rmsg;        /* conn->rmsg: the message being parsed */
+    uint32_t parsed;         /* requests parsed so far (their sequence numbers) */
+    uint32_t *seq;           /* [rb.cap]: sequence number of each deferred request */
+    struct read_batch rb;
+    int waiting;             /* the read batch is submitted and not yet flushed */
+};
+
+struct bs_out {
+    uint32_t *conn, *seq, *single, *idx, *ref;
+    uint32_t n, cap;
+    uint64_t reads, batches, host_keys, polls;
+};
+
+/* req_recv_done's forward, deferred (src/nc_request.c:627-700): what the
+ * reference would do with msg — forward it by key 0 when it makes no
+ * fragments (and is not noforward) — decides `single`; the reference's own
+ * per-message index (server_pool_idx of key 0, as req_forward's
+ * server_pool_conn computes it at :576) is recorded now, beside the batch
+ * site's index recorded at flush */
+static int bs_recv_done(struct bs_conn *bc, struct msg *msg, uint32_t *ref_of_seq, uint32_t ref_cap)
+{
+    const struct server_pool *pool = bc->c.owner;
+    struct msg_tqh frags;
+    TAILQ_INIT(&frags);
+    const uint32_t nk = array_n(msg->keys);
+    int single = 0;
+    if (nk > 0 && !msg->noforward) {
+        const rstatus_t st = msg->fragment(msg, array_n(&pool->server), &frags);
+        single = st == NC_OK && TAILQ_EMPTY(&frags);
+        while (!TAILQ_EMPTY(&frags)) {
+            struct msg *sub = TAILQ_FIRST(&frags);
+            TAILQ_REMOVE(&frags, sub, m_tqe);
+            msg_put(sub);
+        }
+    }
+    if (bc->parsed < ref_cap) {
+        const struct keypos *kp = nk ? array_get(msg->keys, 0) : NULL;
+        ref_of_seq[bc->parsed] = kp ? server_pool_idx(pool, kp->start, (uint32_t)(kp->end - kp->start)) : UINT32_MAX;
+    }
+    bc->seq[bc->rb.n] = bc->parsed++;
+    return read_batch_defer(&bc->rb, msg, single) == NC_OK ? 0 : -1;
+}
+
+/* one read (conn_recv into the last mbuf) and the parse loop of
+ * msg_recv_chain (src/nc_message.c:667-714) with msg_parse / msg_parsed /
+ * msg_repair (:575-661; static there, restated): 0, or -1 */
+static int bs_read(struct bs_conn *bc, uint32_t read_bytes, uint32_t *ref_of_seq, uint32_t ref_cap)
+{
+    struct msg *msg = bc->rmsg;
+    if (msg == NULL) {
+        msg = msg_get(&bc->c, 1, bc->c.redis);
+        if (msg == NULL) return -1;
+        bc->rmsg = msg;
+    }
+    struct mbuf *mbuf = STAILQ_LAST(&msg->mhdr, mbuf, next);
+    if (mbuf == NULL || mbuf_full(mbuf)) {
+        mbuf = mbuf_get();
+        if (mbuf == NULL) return -1;
+        mbuf_insert(&msg->mhdr, mbuf);
+        msg->pos = mbuf->pos;
+    }
+    uint32_t n = (uint32_t)mbuf_size(mbuf);
+    if (n > read_bytes) n = read_bytes;
+    if (n > bc->len - bc->off) n = bc->len - bc->off;
+    memcpy(mbuf->last, bc->stream + bc->off, n);
+    bc->off += n;
+    mbuf->last += n;
+    msg->mlen += n;
+    for (;;) {
+        if (msg_empty(msg)) break;
+        msg->parser(msg);
+        if (msg->result == MSG_PARSE_OK) {
+            struct mbuf *last = STAILQ_LAST(&msg->mhdr, mbuf, next);
+            struct msg *nmsg = NULL;
+            if (msg->pos != last->last) { /* msg_parsed: the unparsed tail becomes the next msg */
+                struct mbuf *nbuf = mbuf_split(&msg->mhdr, msg->pos, NULL, NULL);
+                if (nbuf == NULL) return -1;
+                nmsg = msg_get(msg->owner, msg->request, bc->c.redis);
+                if (nmsg == NULL) {
+                    mbuf_put(nbuf);
+                    return -1;
+                }
+                mbuf_insert(&nmsg->mhdr, nbuf);
+                nmsg->pos = nbuf->pos;
+                nmsg->mlen = mbuf_length(nbuf);
+                msg->mlen -= nmsg->mlen;
+            }
+            bc->rmsg = nmsg;
+            if (bs_recv_done(bc, msg, ref_of_seq, ref_cap) != 0) return -1;
+            if (nmsg == NULL) break;
+            msg = nmsg;
+        } else if (msg->result == MSG_PARSE_REPAIR) { /* msg_repair */
+            struct mbuf *nbuf = mbuf_split(&msg->mhdr, msg->pos, NULL, NULL);
+            if (nbuf == NULL) return -1;
+            mbuf_insert(&msg->mhdr, nbuf);
+            msg->pos = nbuf->pos;
+            break;
+        } else if (msg->result == MSG_PARSE_AGAIN) {
+            break;
+        } else {
+            return -1;
+        }
+    }
+    return 0;
+}
+
+/*
+ * nconn connections, connection c sending stream[soff[c], soff[c+1]); reads
+ * of at most read_bytes. An event loop turns over the connections: a
+ * connection whose read batch is submitted polls it and, once done, forwards
+ * its requests in parse order (recording them in out_*); a connection with
+ * no batch in flight reads and parses its next chunk and submits that read's
+ * batch. Per forwarded request, in forward order: its connection, its
+ * sequence number on that connection, single (1) or not, the batch site's
+ * server index (single) or msg_backend_idx of key 0 (otherwise: the
+ * unchanged path), and the reference's per-message index recorded at parse
+ * time. stats[0..3] = reads, ring batches, keys hashed per key, NC_EAGAIN
+ * polls. Returns the number of requests forwarded, or -1 (parse or set-up
+ * failure), -3 (stalled), -4 (ring error), -5 (output too small).
+ */
+int bs_pipeline(int redis, const uint8_t *stream, const uint64_t *soff, uint32_t nconn, uint32_t read_bytes,
+                int mode, int dist, const char *const *names, const uint32_t *name_lens, const uint32_t *weights,
+                uint32_t nserver, const uint8_t *tag, uint32_t taglen, nc_gpuhash_ring_t *ring, uint32_t *out_conn,
+                uint32_t *out_seq, uint32_t *out_single, uint32_t *out_idx, uint32_t *out_ref, uint32_t cap,
+                uint64_t *stats)
+{
+    struct server_pool pool;
+    if (!rp_ready || nconn == 0) return -1;
+    if (rp_pool_init(&pool, mode, dist, names, name_lens, weights, nserver, tag, taglen) != 0) return -1;
+    const uint32_t rcap = (uint32_t)mbuf_data_size(); /* requests one read can hold, at least */
+    struct bs_conn *bc = calloc(nconn, sizeof(*bc));
+    uint32_t **ref = calloc(nconn, sizeof(*ref));
+    int rc = bc && ref ? 0 : -1;
+    for (uint32_t c = 0; rc == 0 && c < nconn; c++) {
+        bc[c].c.owner = &pool;
+        bc[c].c.client = 1;
+        bc[c].c.redis = redis ? 1 : 0;
+        bc[c].stream = stream + soff[c];
+        bc[c].len = (uint32_t)(soff[c + 1] - soff[c]);
+        bc[c].seq = malloc(rcap * sizeof(uint32_t));
+        ref[c] = malloc((bc[c].len + 1) * sizeof(uint32_t)); /* a request takes >= 1 byte */
+        if (bc[c].seq == NULL || ref[c] == NULL || read_batch_init(&bc[c].rb, &pool, ring, rcap) != NC_OK) rc = -1;
+    }
+    struct bs_out o = {out_conn, out_seq, out_single, out_idx, out_ref, 0, cap, 0, 0, 0, 0};
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int busy = 1; rc == 0 && busy;) {
+        busy = 0;
+        for (uint32_t c = 0; rc == 0 && c < nconn; c++) {
+            struct bs_conn *b = &bc[c];
+            if (b->waiting) {
+                const rstatus_t st = read_batch_poll(&b->rb);
+                if (st == NC_EAGAIN) {
+                    o.polls++;
+                    busy = 1;
+                    continue;
+                }
+                if (st != NC_OK) {
+                    rc = -4;
+                    break;
+                }
+                /* the flush: req_forward of every deferred request, in order */
+                o.batches += b->rb.h.batches;
+                o.host_keys += b->rb.h.host_keys;
+                for (uint32_t i = 0; i < b->rb.n; i++) {
+                    struct msg *m;
+                    uint32_t idx = UINT32_MAX;
+                    const int single = read_batch_server_idx(&b->rb, i, &m, &idx);
+                    if (!single && array_n(m->keys) > 0) {
+                        const struct keypos *kp = array_get(m->keys, 0);
+                        idx = msg_backend_idx(m, kp->start, (uint32_t)(kp->end - kp->start));
+                    }
+                    if (o.n == o.cap) {
+                        rc = -5;
+                        break;
+                    }
+                    o.conn[o.n] = c;
+                    o.seq[o.n] = b->seq[i];
+                    o.single[o.n] = (uint32_t)single;
+                    o.idx[o.n] = idx;
+                    o.ref[o.n] = ref[c][b->seq[i]];
+                    o.n++;
+                    msg_put(m);
+                }
+                read_batch_reset(&b->rb);
+                b->waiting = 0;
+            }
+            if (rc == 0 && b->off < b->len) {
+                if (bs_read(b, read_bytes, ref[c], b->len + 1) != 0) {
+                    rc = -1;
+                    break;
+                }
+                o.reads++;
+                if (read_batch_submit(&b->rb) != NC_OK) {
+                    rc = -4;
+                    break;
+                }
+                b->waiting = 1;
+                busy = 1;
+            }
+        }
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        if (rc == 0 && busy && t1.tv_sec - t0.tv_sec > 20) rc = -3;
+    }
+    for (uint32_t c = 0; bc && c < nconn; c++) {
+        if (bc[c].waiting) { /* a failed run: the teardown rule */
+            read_batch_forget(&bc[c].rb);
+            for (uint32_t i = 0; i < bc[c].rb.n; i++) msg_put(bc[c].rb.msg[i]);
+        }
+        if (bc[c].rmsg) msg_put(bc[c].rmsg);
+        read_batch_deinit(&bc[c].rb);
+        free(bc[c].seq);
+        if (ref) free(ref[c]);
+    }
+    free(bc);
+    free(ref);
+    if (stats) {
+        stats[0] = o.reads;
+        stats[1] = o.batches;
+        stats[2] = o.host_keys;
+        stats[3] = o.polls;
+    }
+    rp_pool_deinit(&pool);
+    return rc == 0 ? (int)o.n : rc;
 }

@@ -139,6 +139,7 @@ SIGNATURES = {
     "nc_gpuhash_ring_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "nc_gpuhash_ring_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "nc_gpuhash_ring_forget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "nc_gpuhash_ring_limits": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "nc_gpuhash_ring_launches": (ctypes.c_uint64, [ctypes.c_void_p]),
     "nc_gpuhash_ring_create_ex": (
         ctypes.c_void_p,

@@ -16,11 +16,28 @@
 
 #include <stdint.h>
 
+#include <atomic>
+
 #include "nc_crc_slice.h"
 #include "nc_direct.h"
 #include "nc_gpuhash.h"
 #include "nc_hash_algo.h"
 #include "nc_hash_key.h"
+
+/* hipFuncSetAttribute(MaxDynamicSharedMemorySize) holds per device: set it
+ * once per kernel and device (the bit of each device already set in `done`)
+ * and report its failure instead of launching into it */
+static inline hipError_t dyn_lds_once(const void *kern, int bytes, std::atomic<uint64_t> &done)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = dev < 64 ? 1ull << dev : 0ull;
+    if (bit != 0u && (done.load(std::memory_order_acquire) & bit) != 0u) return hipSuccess;
+    e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess && bit != 0u) done.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
 
 namespace {
 
@@ -302,7 +319,10 @@ __device__ __forceinline__ uint32_t short_words(const u32x4 (&d)[NC], uint32_t l
             }
         }
         const uint32_t n = len - 12u * nb; /* 1..12 */
-        auto keep = [](uint32_t w, uint32_t m) { return m >= 4u ? w : (w & (0xffffffffu >> (32u - 8u * m))); };
+        /* m = 0 (an empty key) keeps nothing; no shift by 32 (undefined) */
+        auto keep = [](uint32_t w, uint32_t m) {
+            return m >= 4u ? w : (m == 0u ? 0u : (w & (0xffffffffu >> (32u - 8u * m))));
+        };
         a += keep(wa, n);
         if (n > 4u) b += keep(wb, n - 4u);
         if (n > 8u) c += keep(wc, n - 8u);
@@ -553,11 +573,9 @@ hipError_t launch_short_t(const uint8_t *d_keys, const uint64_t *d_off, uint64_t
     constexpr uint32_t kTab = has_table<MODE>() ? nc_slice::table_words<R, 4u * NW>() * 4u : 0u;
     const uint32_t pad = kTab >= 90112u ? 0u : 90112u - kTab;
     auto k = nc_bytes_short_kernel<MODE, NC, DEPTH, kW, NW, R>;
-    static const bool attr = [&] { /* once per instantiation (and process: one device kind) */
-        (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad);
-        return true;
-    }();
-    (void)attr;
+    static std::atomic<uint64_t> attr_done{0}; /* per instantiation: the devices it is set on */
+    const hipError_t ea = dyn_lds_once((const void *)k, (int)pad, attr_done);
+    if (ea != hipSuccess) return ea;
     (void)hipGetLastError();
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * kW), pad, stream, d_keys, d_off, nkeys, d_out, ntiles);
     return hipGetLastError();
@@ -626,9 +644,12 @@ hipError_t launch_opt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nke
             }
         }
         const uint32_t pad = has_table<MODE>() ? 0u : 40960u;
-        if (pad)
-            (void)hipFuncSetAttribute((const void *)nc_bytes_direct_kernel<MODE, true, true, 8, OPT>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad);
+        if (pad) {
+            static std::atomic<uint64_t> attr_done{0};
+            const hipError_t ea =
+                dyn_lds_once((const void *)nc_bytes_direct_kernel<MODE, true, true, 8, OPT>, (int)pad, attr_done);
+            if (ea != hipSuccess) return ea;
+        }
         hipLaunchKernelGGL((nc_bytes_direct_kernel<MODE, true, true, 8, OPT>), dim3((unsigned)grid8), dim3(512), pad,
                            stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
         return hipGetLastError();

@@ -576,7 +576,12 @@ extern "C" rstatus_t nc_gpuhash_ring_submit_spans(nc_gpuhash_ring_t *r, int mode
     const uint64_t seq = r->seq;
     const uint32_t s = (uint32_t)(seq % r->nslots), g = (uint32_t)(seq % r->nlanes);
     if (!ring_reap(r, s)) {
+        /* the slot's batch still runs — or waits for a worker: its lane may
+         * have left with nobody polling the ticket (forgotten), so relaunch
+         * here as a poll would */
+        const rstatus_t rc = ring_ensure_worker(r, (uint32_t)(r->slot_seq[s] % r->nlanes));
         pthread_mutex_unlock(&r->lock);
+        if (rc != NC_OK) return rc;
         errno = EAGAIN;
         return NC_EAGAIN;
     }
@@ -720,6 +725,19 @@ extern "C" rstatus_t nc_gpuhash_ring_debug_hold(nc_gpuhash_ring_t *r, int hold)
 }
 
 extern "C" uint32_t nc_gpuhash_ring_lanes(const nc_gpuhash_ring_t *r) { return r ? r->nlanes : 0; }
+
+extern "C" rstatus_t nc_gpuhash_ring_limits(const nc_gpuhash_ring_t *r, uint32_t *max_keys, uint64_t *max_key_bytes,
+                                            uint32_t *nslots)
+{
+    if (r == NULL) {
+        errno = EINVAL;
+        return NC_ERROR;
+    }
+    if (max_keys) *max_keys = r->max_keys;
+    if (max_key_bytes) *max_key_bytes = r->max_key_bytes;
+    if (nslots) *nslots = r->nslots;
+    return NC_OK;
+}
 
 extern "C" rstatus_t nc_gpuhash_ring_debug_timeline(nc_gpuhash_ring_t *r, int on, uint32_t slot, uint64_t out[8])
 {
