@@ -36,6 +36,25 @@ rstatus_t nc_gpuhash_probe_read_nt(const void *d_buf, uint64_t bytes, uint32_t *
 rstatus_t nc_gpuhash_probe_mix(const void *d_buf, uint64_t bytes, void *d_wout, uint64_t wout_bytes,
                                uint32_t *d_sink, void *stream, int policy, int iters, float *avg_ms);
 
+/* The grouped C2 pipeline's store pattern against its reads (VERDICT r05
+ * item 5): tiles of tile_read contiguous bytes (a multiple of 8 KiB) read
+ * with nt 16-byte loads by 512-thread workgroups (`grid` of them, tiles
+ * grid-strided in runs of `run` consecutive tiles), each tile's tile_write
+ * output bytes at d_out + tile * tile_write — stored after its tile, or
+ * (defer) once per run from LDS, run * tile_write <= 8 KiB contiguous.
+ * Mean ms per pass of all bytes / tile_read tiles. */
+rstatus_t nc_gpuhash_probe_tile_mix(const void *d_buf, uint64_t bytes, void *d_out, uint64_t out_bytes,
+                                   uint32_t tile_read, uint32_t tile_write, uint32_t run, uint32_t grid, int defer,
+                                   uint32_t *d_sink, void *stream, int iters, float *avg_ms);
+
+/* Clock sampler: ONE wave on `stream` (launched before the kernels it
+ * watches, so it holds its slot) records n samples of (s_memtime,
+ * s_memrealtime) into d_out[2n], one every gap_ticks of the 100 MHz
+ * real-time clock, then exits (n * gap_ticks <= 1 s). Asynchronous: the
+ * shader clock the GPU ran at while the other streams' kernels ran is
+ * (c[i+1] - c[i]) / (r[i+1] - r[i]) * 100 MHz (tools/clock_probe.py). */
+rstatus_t nc_gpuhash_probe_clock_sampler(uint64_t *d_out, uint32_t n, uint32_t gap_ticks, void *stream);
+
 /* The launch variant the auto policy picks for this mode and shape (the
  * variant bits of nc_gpuhash_set_tuning; bit 16 = the plain workgroup
  * pipeline); -1 with errno EINVAL for an invalid mode. */

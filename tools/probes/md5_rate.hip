@@ -102,8 +102,15 @@ __device__ __forceinline__ void steps(uint32_t (&v)[4], const uint32_t (&w)[16],
 }
 
 template <int FORM>
-__global__ __launch_bounds__(256) void md5_rounds(unsigned *out, int rounds)
+__global__ __launch_bounds__(256) void md5_rounds(unsigned *out, int rounds, unsigned long long *clk)
 {
+    /* workgroup 0 (resident the whole launch: the grid is one wave set)
+     * stamps the shader clock and the 100 MHz real-time clock at its start
+     * and end: the clock this launch ran at */
+    if (clk != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+        clk[0] = __builtin_readcyclecounter();
+        clk[1] = wall_clock64();
+    }
     uint32_t w[16];
 #pragma unroll
     for (int t = 0; t < 16; t++) w[t] = threadIdx.x * 0x9e3779b9u + t;
@@ -122,27 +129,51 @@ __global__ __launch_bounds__(256) void md5_rounds(unsigned *out, int rounds)
         w[r & 15] ^= acc; /* keeps the rounds dependent on each other's data */
     }
     if (acc == 0x12345678u) out[blockIdx.x] = acc;
+    if (clk != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        clk[2] = __builtin_readcyclecounter();
+        clk[3] = wall_clock64();
+    }
 }
 
+/* sustain_ms > 0: launches back to back for that long first (the power
+ * controller settles the clock under a long VALU-bound load, as under the
+ * hash kernels' timed loops), then times 10 more */
 template <int FORM>
-static void run(int wps, unsigned *o, int cus)
+static void run(int wps, unsigned *o, int cus, unsigned long long *clk, double sustain_ms = 0.0)
 {
     const int rounds = 256;
     const int blocks = cus * wps;
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
-    for (int i = 0; i < 3; i++) hipLaunchKernelGGL(md5_rounds<FORM>, dim3(blocks), dim3(256), 0, 0, o, rounds);
+    for (int i = 0; i < 3; i++) hipLaunchKernelGGL(md5_rounds<FORM>, dim3(blocks), dim3(256), 0, 0, o, rounds, nullptr);
+    if (sustain_ms > 0.0) {
+        float el = 0.f;
+        (void)hipEventRecord(a, 0);
+        while (el < sustain_ms) {
+            for (int i = 0; i < 20; i++)
+                hipLaunchKernelGGL(md5_rounds<FORM>, dim3(blocks), dim3(256), 0, 0, o, rounds, nullptr);
+            (void)hipEventRecord(b, 0);
+            (void)hipEventSynchronize(b);
+            (void)hipEventElapsedTime(&el, a, b);
+        }
+    }
     (void)hipEventRecord(a, 0);
-    for (int i = 0; i < 10; i++) hipLaunchKernelGGL(md5_rounds<FORM>, dim3(blocks), dim3(256), 0, 0, o, rounds);
+    for (int i = 0; i < 10; i++)
+        hipLaunchKernelGGL(md5_rounds<FORM>, dim3(blocks), dim3(256), 0, 0, o, rounds, i == 9 ? clk : nullptr);
     (void)hipEventRecord(b, 0);
     (void)hipEventSynchronize(b);
     float ms;
     (void)hipEventElapsedTime(&ms, a, b);
     ms /= 10;
+    unsigned long long c[4] = {0, 0, 0, 0};
+    (void)hipMemcpy(c, clk, sizeof c, hipMemcpyDeviceToHost);
+    const double mhz = c[3] > c[1] ? (double)(c[2] - c[0]) / (double)(c[3] - c[1]) * 100.0 : 0.0;
     const double ns_per_round = ms * 1e6 / ((double)wps * rounds);
-    printf("{\"form\": %d, \"waves_per_simd\": %d, \"ms\": %.4f, \"ns_per_round_per_simd\": %.2f, \"c3_ms\": %.4f}\n",
-           FORM, wps, ms, ns_per_round, ns_per_round * 1024 * 1e-6);
+    printf("{\"form\": %d, \"waves_per_simd\": %d, \"sustained\": %s, \"ms\": %.4f, \"ns_per_round_per_simd\": %.2f, "
+           "\"c3_ms\": %.4f, \"clock_mhz\": %.1f}\n",
+           FORM, wps, sustain_ms > 0.0 ? "true" : "false", ms, ns_per_round, ns_per_round * 1024 * 1e-6, mhz);
 }
 
 template <int FORM>
@@ -171,6 +202,8 @@ int main()
     (void)hipGetDeviceProperties(&p, 0);
     unsigned *o;
     (void)hipMalloc(&o, 1 << 20);
+    unsigned long long *clk;
+    (void)hipMalloc(&clk, 64);
     {
         unsigned h0[256], h5[256], h6[256], h7[256];
         hipLaunchKernelGGL(md5_check<0>, dim3(1), dim3(64), 0, 0, o);
@@ -191,14 +224,17 @@ int main()
                bad ? "false" : "true", bad, bad6, bad7);
     }
     for (int wps : {4, 8}) {
-        run<0>(wps, o, p.multiProcessorCount);
-        run<1>(wps, o, p.multiProcessorCount);
-        run<2>(wps, o, p.multiProcessorCount);
-        run<3>(wps, o, p.multiProcessorCount);
-        run<4>(wps, o, p.multiProcessorCount);
-        run<5>(wps, o, p.multiProcessorCount);
-        run<6>(wps, o, p.multiProcessorCount);
-        run<7>(wps, o, p.multiProcessorCount);
+        run<0>(wps, o, p.multiProcessorCount, clk);
+        run<1>(wps, o, p.multiProcessorCount, clk);
+        run<2>(wps, o, p.multiProcessorCount, clk);
+        run<3>(wps, o, p.multiProcessorCount, clk);
+        run<4>(wps, o, p.multiProcessorCount, clk);
+        run<5>(wps, o, p.multiProcessorCount, clk);
+        run<6>(wps, o, p.multiProcessorCount, clk);
+        run<7>(wps, o, p.multiProcessorCount, clk);
     }
+    /* the kernel's form at 8 waves per SIMD after 300 ms of back-to-back
+     * launches: the rate at the clock a long md5 load settles at */
+    run<0>(8, o, p.multiProcessorCount, clk, 300.0);
     return 0;
 }

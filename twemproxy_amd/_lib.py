@@ -139,6 +139,12 @@ SIGNATURES = {
     "nc_gpuhash_ring_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "nc_gpuhash_ring_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "nc_gpuhash_ring_forget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "nc_gpuhash_probe_tile_mix": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_float)]),
+    "nc_gpuhash_probe_clock_sampler": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                                      ctypes.c_void_p]),
     "nc_gpuhash_ring_limits": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "nc_gpuhash_ring_launches": (ctypes.c_uint64, [ctypes.c_void_p]),
     "nc_gpuhash_ring_create_ex": (
