@@ -261,7 +261,11 @@ def md5_ops(torch, off) -> float:
     return float(((lens + 8) // 64 + 1).sum().item()) * MD5_OPS_PER_BLOCK
 
 
-def valu_roofline(ops: float, kern_ms: float, ceiling):
+def valu_roofline(ops: float, kern_ms: float, ceiling, clock_mhz=None):
+    """md5's VALU roofline; with the clock the leg ran at (clock_under) also
+    the ceiling scaled to that clock: the probe's rate x clock / the probe's
+    own clock (the probe, VALU alone, holds ~2.37 GHz; the hash kernels,
+    VALU under HBM traffic, run at 1.9-2.2 GHz)"""
     achieved = ops / (kern_ms * 1e-3)
     r = {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(VALU_PEAK / 1e12, 3),
          "unit": "Tlane-op/s", "frac": round(achieved / VALU_PEAK, 4), "alg_ops_per_launch": int(ops),
@@ -269,7 +273,66 @@ def valu_roofline(ops: float, kern_ms: float, ceiling):
     if ceiling:
         r["md5_compute_ceiling"] = ceiling
         r["frac_of_md5_compute_ceiling"] = round(achieved / (ceiling["tlane_ops_s"] * 1e12), 4)
+    if clock_mhz:
+        r["clock_mhz"] = clock_mhz
+        r["frac_of_peak_at_clock"] = round(achieved / (VALU_PEAK * clock_mhz / 2400.0), 4)
+        if ceiling and ceiling.get("clock_mhz"):
+            r["frac_of_md5_compute_ceiling_at_clock"] = round(
+                achieved / (ceiling["tlane_ops_s"] * 1e12 * clock_mhz / ceiling["clock_mhz"]), 4)
     return r
+
+
+def clock_under(t, torch, launch, samples=3000, gap=2000, tries=4):
+    """Median shader clock (MHz) while `launch(stream)` runs back to back:
+    one sampler wave (nc_gpuhash_probe_clock_sampler, launched first on its
+    own high-priority stream) stamps s_memtime against the 100 MHz
+    s_memrealtime every 20 us for 60 ms. Run after a leg's timed region,
+    never inside it: md5 runs below the 2.4 GHz the VALU peak assumes (the
+    board's power limit under VALU + HBM load, profiles/r06c_clock.json), and
+    its compute ceiling is read at the clock it actually ran at. Two streams
+    can land on one hardware queue, where the work would wait for the
+    sampler and the sampler would see an idle GPU: a window the work did not
+    fill (fewer launches than the window holds) is measured again on fresh
+    streams; None if no try overlapped."""
+    from twemproxy_amd import _lib as L
+
+    dev = torch.cuda.current_device()
+    buf = torch.zeros(2 * samples, dtype=torch.int64, device=dev)
+    for attempt in range(tries):
+        s_samp = torch.cuda.Stream(priority=-1)
+        s_work = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        L.check(L.lib().nc_gpuhash_probe_clock_sampler(buf.data_ptr(), samples, gap, s_samp.cuda_stream),
+                "nc_gpuhash_probe_clock_sampler")
+        done = torch.cuda.Event()
+        done.record(s_samp)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s_work)
+        t0 = time.perf_counter()
+        n = 0
+        while not done.query() and time.perf_counter() - t0 < 5.0:
+            with torch.cuda.stream(s_work):
+                for _ in range(4):
+                    launch(s_work)
+                    n += 1
+            s_work.synchronize()
+        e1.record(s_work)
+        torch.cuda.synchronize()
+        a = buf.cpu().numpy().astype(np.int64)
+        dc, dr = np.diff(a[0::2]), np.diff(a[1::2])
+        window_ms = float(a[-1] - a[1]) / 1e5
+        work_ms = e0.elapsed_time(e1)
+        mhz = dc[dr > 0] / dr[dr > 0] * 100.0
+        mid = mhz[int(0.1 * mhz.size): int(0.9 * mhz.size)]
+        med = float(np.median(mid if mid.size else mhz))
+        # the work must have been running for the whole window, and longer:
+        # launches only stop once the sampler is done
+        ok = n > 8 and work_ms >= 0.9 * window_ms
+        log(f"clock_under try {attempt}: {n} launches over {work_ms:.1f} ms, window {window_ms:.1f} ms, "
+            f"median {med:.1f} MHz{'' if ok else ' (no overlap: again)'}")
+        if ok:
+            return round(med, 1)
+    return None
 
 
 def md5_ceiling():
@@ -290,9 +353,12 @@ def md5_ceiling():
         return None
     # one round = 64 lanes x one 61-step final block (61 x 5 ops + 1 add)
     ops = 64 * (61 * 5 + 1)
-    return {"tlane_ops_s": round(ops * 1024 / (best["ns_per_round_per_simd"] * 1e-9) / 1e12, 3),
-            "source": f"tools/probes/md5_rate.hip (fastest of its step forms: form {best['form']}, "
-                      f"{best['waves_per_simd']} waves/SIMD)"}
+    c = {"tlane_ops_s": round(ops * 1024 / (best["ns_per_round_per_simd"] * 1e-9) / 1e12, 3),
+         "source": f"tools/probes/md5_rate.hip (fastest of its step forms: form {best['form']}, "
+                   f"{best['waves_per_simd']} waves/SIMD{', after 300 ms of sustained load' if best.get('sustained') else ''})"}
+    if best.get("clock_mhz"):
+        c["clock_mhz"] = best["clock_mhz"]
+    return c
 
 
 def read_ceiling(t, rf, buf):
@@ -572,7 +638,9 @@ def main():
         m = leg(t, torch, "md5", keys, off, out, s5, 1, dist_on, shape, key_bytes, nk, key_bytes,
                 "C2 keys, md5", "C2")
         m["roofline_hbm"] = m.pop("roofline")
-        m["roofline"] = valu_roofline(md5_ops(torch, off), m["kernel_ms"], ceiling)  # md5's binding ceiling
+        clk = clock_under(t, torch, lambda st: t.hash_batch_device("md5", keys, off, out, stream=st, shape=shape,
+                                                                   key_end=key_bytes))
+        m["roofline"] = valu_roofline(md5_ops(torch, off), m["kernel_ms"], ceiling, clk)  # md5's binding ceiling
         res["md5"] = m
         check("C2", "md5", out, first, nk, n_local)
         # ---- fused server_pool_idx: fnv1a_64 + ketama_dispatch over
@@ -620,7 +688,9 @@ def main():
         m3 = leg(t, torch, "md5", keys3, off3, out3, max(5, args.steps // 2), 1, dist_on, sh3, kb3, nk3, kb3,
                  f"C3: md5 over {n_local} x 32 B keys per GPU", "C3")
         m3["roofline_hbm"] = m3.pop("roofline")
-        m3["roofline"] = valu_roofline(md5_ops(torch, off3), m3["kernel_ms"], ceiling)
+        clk3 = clock_under(t, torch, lambda st: t.hash_batch_device("md5", keys3, off3, out3, stream=st, shape=sh3,
+                                                                    key_end=kb3))
+        m3["roofline"] = valu_roofline(md5_ops(torch, off3), m3["kernel_ms"], ceiling, clk3)
         res["c3_md5"] = m3
         check("C3", "md5", out3, first3, nk3, n_local)
         if sc3:
@@ -642,7 +712,9 @@ def main():
             x = leg(t, torch, mode, keys4, off4, out4, 10, 1, dist_on, sh4, kb4, nk4, kb4, mode, "C4")
             x.pop("workload")
             if mode == "md5":
-                x["roofline_valu"] = valu_roofline(md5_ops(torch, off4), x["kernel_ms"], ceiling)
+                clk4 = clock_under(t, torch, lambda st: t.hash_batch_device("md5", keys4, off4, out4, stream=st,
+                                                                            shape=sh4, key_end=kb4))
+                x["roofline_valu"] = valu_roofline(md5_ops(torch, off4), x["kernel_ms"], ceiling, clk4)
             r4[mode] = x
             check("C4", mode, out4, first4, nk4, n4)
         if sc4:
@@ -716,7 +788,8 @@ def main():
 NORTH_STAR_FRAC = 0.70  # BASELINE.json north_star: >= 70 % of HBM peak on C3 fnv1a_64
 
 
-def _rf(r: dict | None, keep=("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_over_alg")) -> dict | None:
+def _rf(r: dict | None, keep=("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_over_alg",
+                              "clock_mhz", "frac_of_md5_compute_ceiling_at_clock")) -> dict | None:
     if r is None:
         return None
     return {k: r[k] for k in keep if k in r}
@@ -733,7 +806,8 @@ def _leg(x: dict | None, extra=()) -> dict | None:
         s["roofline"] = _rf(x["roofline"])
     for k in extra:
         if k in x:
-            s[k] = _rf(x[k], ("bound", "frac", "traffic_over_alg", "frac_of_md5_compute_ceiling"))
+            s[k] = _rf(x[k], ("bound", "frac", "traffic_over_alg", "frac_of_md5_compute_ceiling", "clock_mhz",
+                              "frac_of_md5_compute_ceiling_at_clock"))
     return s
 
 
@@ -759,7 +833,8 @@ def summarize(res: dict, detail_path: str | None) -> dict:
         line["md5"] = _leg(res["md5"], ("roofline_hbm",))
         if "roofline" in res["md5"]:
             line["md5"]["roofline"] = _rf(res["md5"]["roofline"], ("bound", "achieved", "peak", "unit", "frac",
-                                                                    "frac_of_md5_compute_ceiling"))
+                                                                    "frac_of_md5_compute_ceiling", "clock_mhz",
+                                                                    "frac_of_md5_compute_ceiling_at_clock"))
     if "server_idx_ketama" in res:
         s = _leg(res["server_idx_ketama"])
         if "kernel_ms" in s and res.get("kernel_ms_rank0"):
