@@ -11,7 +11,8 @@ rank 0 generates all N x 2^26 keys and scatters byte-balanced ranges over
 RCCL (grouped point-to-point); scatter time is reported separately and is
 not part of `value` (weak scaling: fixed keys per GPU).
 
-Rank 0 prints ONE JSON line (a summary under ~5 KB; the full record goes to
+Rank 0 prints ONE JSON line (a summary whose last ~1800 characters hold every
+kernel leg and the north-star object; the full record goes to
 --detail-out). `value` = total keys hashed by all ranks per
 second (Mkeys/s) over K timed steps, max over ranks. Beside it, each timed
 with HIP events on the launch stream:
@@ -51,8 +52,16 @@ SPINUP_S = 0.5  # untimed launches before the warm-up steps (clock ramp)
 METRIC = "Mkeys/s + GB/s hashed (device-resident), fnv1a_64 & md5, 1/2/4/8 MI355X"
 
 
+VERBOSE = False  # --verbose: progress notes on stderr (the driver's 2000-character tail takes stderr too)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def note(*a):
+    if VERBOSE:
+        log(*a)
 
 
 def parse():
@@ -75,7 +84,11 @@ def parse():
     p.add_argument("--detail-out", default=None,
                    help="where rank 0 writes the full record (default gpurun_out/bench_detail.json when that "
                         "directory exists); the printed line is its summary")
-    return p.parse_args()
+    p.add_argument("--verbose", action="store_true", help="progress notes on stderr")
+    a = p.parse_args()
+    global VERBOSE
+    VERBOSE = a.verbose
+    return a
 
 
 def _free_port() -> int:
@@ -328,7 +341,7 @@ def clock_under(t, torch, launch, samples=3000, gap=2000, tries=4):
         # the work must have been running for the whole window, and longer:
         # launches only stop once the sampler is done
         ok = n > 8 and work_ms >= 0.9 * window_ms
-        log(f"clock_under try {attempt}: {n} launches over {work_ms:.1f} ms, window {window_ms:.1f} ms, "
+        note(f"clock_under try {attempt}: {n} launches over {work_ms:.1f} ms, window {window_ms:.1f} ms, "
             f"median {med:.1f} MHz{'' if ok else ' (no overlap: again)'}")
         if ok:
             return round(med, 1)
@@ -788,69 +801,56 @@ def main():
 NORTH_STAR_FRAC = 0.70  # BASELINE.json north_star: >= 70 % of HBM peak on C3 fnv1a_64
 
 
-def _rf(r: dict | None, keep=("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_over_alg",
-                              "clock_mhz", "frac_of_md5_compute_ceiling_at_clock")) -> dict | None:
+TAIL_CHARS = 1800  # the driver keeps the last 2000 characters of stdout + stderr
+
+
+def _rf(r: dict | None, keep=("bound", "frac", "traffic_over_alg", "clock_mhz",
+                              "frac_of_md5_compute_ceiling_at_clock")) -> dict | None:
     if r is None:
         return None
     return {k: r[k] for k in keep if k in r}
 
 
 def _leg(x: dict | None, extra=()) -> dict | None:
-    """one leg of the full record, cut to what a reader of the line needs"""
+    """one leg of the full record, cut to kernel time and roofline fraction
+    (rate, achieved/peak/traffic stay in the detail file)"""
     if x is None:
         return None
     if "error" in x:
         return {"error": x["error"][:200]}
-    s = {k: x[k] for k in ("kernel_ms", "value", "unit") if k in x}
+    s = {k: x[k] for k in ("kernel_ms",) if k in x}
     if "roofline" in x:
         s["roofline"] = _rf(x["roofline"])
     for k in extra:
         if k in x:
-            s[k] = _rf(x[k], ("bound", "frac", "traffic_over_alg", "frac_of_md5_compute_ceiling", "clock_mhz",
-                              "frac_of_md5_compute_ceiling_at_clock"))
+            s[k] = _rf(x[k])
     return s
 
 
 def summarize(res: dict, detail_path: str | None) -> dict:
-    """The printed line: the driver's contract fields, the headline roofline
-    and cpu_baseline, then every leg cut to kernel time, value and roofline
-    fraction (the whole record, per-depth C5 rows and ceilings included, goes
-    to `detail_path`). The driver keeps the last ~8 KB of stdout, so the line
-    must stay well under that; the north-star figure and the C2 md5 leg come
-    right after the headline."""
+    """The printed line. The driver parses the whole line but keeps only the
+    last ~2000 characters of output in its record, so the order is: the
+    contract fields, the headline roofline, cpu_baseline, parity and the
+    end-to-end legs first; then every kernel leg cut to kernel time, rate and
+    roofline fraction, ending with the C2 md5 leg, C3 fnv1a_64 and the
+    north-star object, so that the record's tail holds all of them
+    (`TAIL_CHARS`, checked by tests/test_bench_line.py). The whole record,
+    per-depth C5 rows and ceilings included, goes to `detail_path`."""
     line = {k: res[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
                                 "gb_per_s_hashed", "kernel_ms_rank0", "kernel_ms_max", "variant", "roofline")
             if k in res}
-    c3 = res.get("c3_fnv1a_64")
-    if c3 and "roofline" in c3:
-        rf = c3["roofline"]
-        line["north_star"] = {"workload": "C3 fnv1a_64 (BASELINE configs[2])", "kernel_ms": c3["kernel_ms"],
-                              "frac": rf["frac"], "target_frac": NORTH_STAR_FRAC,
-                              "met": rf["frac"] >= NORTH_STAR_FRAC, "traffic": rf.get("traffic"),
-                              "traffic_over_alg": rf.get("traffic_over_alg")}
-    if "md5" in res:
-        line["md5"] = _leg(res["md5"], ("roofline_hbm",))
-        if "roofline" in res["md5"]:
-            line["md5"]["roofline"] = _rf(res["md5"]["roofline"], ("bound", "achieved", "peak", "unit", "frac",
-                                                                    "frac_of_md5_compute_ceiling", "clock_mhz",
-                                                                    "frac_of_md5_compute_ceiling_at_clock"))
-    if "server_idx_ketama" in res:
-        s = _leg(res["server_idx_ketama"])
-        if "kernel_ms" in s and res.get("kernel_ms_rank0"):
-            s["over_hash"] = round(s["kernel_ms"] / res["kernel_ms_rank0"] - 1.0, 4)
-        line["server_idx_ketama"] = s
-    for k in ("c3_fnv1a_64", "c3_crc32", "c3_md5"):
-        if k in res:
-            line[k] = _leg(res[k], ("roofline_lds", "roofline_hbm"))
-    if "c4_shard" in res:
-        c4 = res["c4_shard"]
-        line["c4_shard"] = {m: _leg(c4[m], ("roofline_valu",)) for m in ("md5", "crc32", "fnv1a_64") if m in c4}
-        if "scatter" in c4:
-            line["c4_shard"]["scatter"] = c4["scatter"]
-    for k in ("scatter", "c3_scatter"):
-        if k in res:
-            line[k] = res[k]
+    if "cpu_baseline" in res:
+        cb = res["cpu_baseline"]
+        line["cpu_baseline"] = cb if "error" in cb else {
+            **{k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "threads_share", "cpu_model")},
+            "mkeys_s_1thread": cb["detail"]["fnv1a_64"].get("mkeys_s_1threads"),
+            "md5_mkeys_s_all_cores": cb["detail"].get("md5", {}).get(f"mkeys_s_{cb['cores']}threads")}
+    par = res["parity"]
+    line["parity"] = {"all": par["all"], "legs": len(par["per_rank"]),
+                      "ranks": max((len(v) for v in par["per_rank"].values()), default=0),
+                      "bad": sorted(k for k, v in par["per_rank"].items() if any(x not in ("ok", "unpinned") for x in v))}
+    line["detail"] = detail_path
     r = res.get("redis_key_extraction")
     if r:
         line["redis_key_extraction"] = r if "error" in r else {k: r[k] for k in ("ms_per_parse_wall", "mreq_s")}
@@ -865,23 +865,40 @@ def summarize(res: dict, detail_path: str | None) -> dict:
             line["c5_e2e"] = c5
         else:
             def pt(r_):
-                return None if r_ is None else {k: r_[k] for k in ("path", "depth", "lanes", "submit_to_done_us",
+                return None if r_ is None else {k: r_[k] for k in ("depth", "lanes", "submit_to_done_us",
                                                                    "us_per_batch", "mkeys_s") if k in r_}
             ring1 = next((r_ for r_ in c5["gpu"] if r_["path"].startswith("ring") and r_["depth"] == 1), None)
             line["c5_e2e"] = {"host_per_key": pt(c5["host_per_key"]), "ring_depth1": pt(ring1),
                               "ring_best_depth_ge2_le20us": pt(c5["ring_best_depth_ge2_le20us"]),
                               "points": len(c5["gpu"]), "mismatches": c5["mismatches"]}
-    if "cpu_baseline" in res:
-        cb = res["cpu_baseline"]
-        line["cpu_baseline"] = cb if "error" in cb else {
-            **{k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "threads_share", "cpu_model")},
-            "mkeys_s_1thread": cb["detail"]["fnv1a_64"].get("mkeys_s_1threads"),
-            "md5_mkeys_s_all_cores": cb["detail"].get("md5", {}).get(f"mkeys_s_{cb['cores']}threads")}
-    par = res["parity"]
-    line["parity"] = {"all": par["all"], "legs": len(par["per_rank"]),
-                      "ranks": max((len(v) for v in par["per_rank"].values()), default=0),
-                      "bad": sorted(k for k, v in par["per_rank"].items() if any(x not in ("ok", "unpinned") for x in v))}
-    line["detail"] = detail_path
+    for k in ("scatter", "c3_scatter"):
+        if k in res:
+            line[k] = res[k]
+    # ---- the kernel legs: these make up the record's tail
+    if "c4_shard" in res:
+        c4 = res["c4_shard"]
+        line["c4_shard"] = {m: _leg(c4[m], ("roofline_valu",)) for m in ("md5", "crc32", "fnv1a_64") if m in c4}
+        if "scatter" in c4:
+            line["c4_shard"]["scatter"] = c4["scatter"]
+    for k in ("c3_md5", "c3_crc32"):
+        if k in res:
+            line[k] = _leg(res[k], ("roofline_lds", "roofline_hbm"))
+    if "server_idx_ketama" in res:
+        s = _leg(res["server_idx_ketama"])
+        if "kernel_ms" in s and res.get("kernel_ms_rank0"):
+            s["over_hash"] = round(s["kernel_ms"] / res["kernel_ms_rank0"] - 1.0, 4)
+        line["server_idx_ketama"] = s
+    if "md5" in res:
+        line["md5"] = _leg(res["md5"], ("roofline_hbm",))
+    if "c3_fnv1a_64" in res:
+        line["c3_fnv1a_64"] = _leg(res["c3_fnv1a_64"])
+    c3 = res.get("c3_fnv1a_64")
+    if c3 and "roofline" in c3:
+        rf = c3["roofline"]
+        line["north_star"] = {"workload": "C3 fnv1a_64", "kernel_ms": c3["kernel_ms"],
+                              "frac": rf["frac"], "target_frac": NORTH_STAR_FRAC,
+                              "met": rf["frac"] >= NORTH_STAR_FRAC, "traffic": rf.get("traffic"),
+                              "traffic_over_alg": rf.get("traffic_over_alg")}
     return line
 
 
