@@ -14,17 +14,33 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
 
 @pytest.fixture(scope="module")
-def line():
+def run(tmp_path_factory):
     import torch  # noqa: F401  (pages the image in before the child's own import)
 
+    detail = str(tmp_path_factory.mktemp("bench") / "detail.json")
     cmd = [sys.executable, "-u", os.path.join(HERE, "bench.py"), "--steps", "3", "--warmup", "1",
-           "--nkeys", str(1 << 20), "--c4-nkeys", str(1 << 16), "--cpu-sample", str(1 << 16)]
+           "--nkeys", str(1 << 20), "--c4-nkeys", str(1 << 16), "--cpu-sample", str(1 << 16), "--detail-out", detail]
     p = subprocess.run(cmd, cwd=HERE, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     rows = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(rows) == 1, p.stdout[-2000:]
-    assert len(rows[0]) < 6000  # the driver keeps ~8 KB of stdout: the whole line must survive
-    return json.loads(rows[0])
+    # the driver keeps the last 2000 characters of stdout + stderr: the line
+    # ends with every kernel leg, and a plain run writes nothing on stderr
+    # beyond the runtime's own notices
+    assert len(p.stderr) < 600, p.stderr[-1000:]
+    return rows[0], json.load(open(detail))
+
+
+@pytest.fixture(scope="module")
+def line(run):
+    return json.loads(run[0])
+
+
+def test_tail_holds_every_leg(run):
+    tail = run[0][-1800:]
+    for k in ('"c4_shard":', '"c3_md5":', '"c3_crc32":', '"server_idx_ketama":', '"md5":', '"c3_fnv1a_64":',
+              '"north_star":'):
+        assert k in tail, k
 
 
 def test_driver_fields(line):
@@ -69,7 +85,15 @@ def test_secondary_legs(line):
         assert line[k]["kernel_ms"] > 0
     for mode in ("md5", "crc32", "fnv1a_64"):
         assert line["c4_shard"][mode]["kernel_ms"] > 0
-        assert line["c4_shard"][mode]["roofline"]["traffic"] is None
+        # no PMC traffic borrowed from the full-size profiles, in the line or the detail file
+        assert "traffic_over_alg" not in line["c4_shard"][mode]["roofline"]
+
+
+def test_detail_record(run):
+    detail = run[1]
+    for mode in ("md5", "crc32", "fnv1a_64"):
+        assert detail["c4_shard"][mode]["roofline"]["traffic"] is None
+    assert len(detail["c5_e2e"]["gpu"]) >= 2
 
 
 def test_north_star_and_summary(line):
