@@ -40,9 +40,18 @@ def is_hash_kernel(name):
 
 
 def hash_phases(trace_csv):
-    """consecutive runs of nc_hash_kernel dispatches, split where another kernel runs"""
+    """consecutive runs of nc_hash_kernel dispatches, split where another kernel
+    runs; the launches bench.py's clock_under makes beside the clock sampler
+    (after a leg's timed region, round 6) are dropped, sampler included"""
     rows = list(csv.DictReader(open(trace_csv)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    samp = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if "clock_sampler" in r["Kernel_Name"]]
+
+    def beside_sampler(r):
+        t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        return any(a <= t1 and t0 <= b for a, b in samp)
+
+    rows = [r for r in rows if "clock_sampler" not in r["Kernel_Name"] and not beside_sampler(r)]
     runs, cur = [], None
     for r in rows:
         name = r["Kernel_Name"]
@@ -121,7 +130,9 @@ def main():
 
     bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
     under = json.loads(open(os.path.join(src, "bench_under_rocprof.json")).read().strip().splitlines()[-1])
-    runs = hash_phases(os.path.join(prof, "bench_kernel_trace.csv"))
+    # (a launch or two of clock_under's that started before its sampler can
+    # remain as a short run of its own: no leg has fewer than 5 dispatches)
+    runs = [r for r in hash_phases(os.path.join(prof, "bench_kernel_trace.csv")) if len(r["ns"]) >= 5]
     # the device-resident legs come first; the end-to-end legs after them
     # launch the hash kernel per chunk, between copies (more runs)
     if len(runs) < len(BENCH_PHASES):

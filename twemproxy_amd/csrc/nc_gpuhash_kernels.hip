@@ -1958,6 +1958,7 @@ constexpr int kVarDirect8 = 1 << 12;     /* line image: eight-wave workgroups, o
 constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
 constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
 constexpr int kVarMd5PadTab = 1 << 15;    /* md5: padding selectors from an LDS table */
+[[maybe_unused]] constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores */
 constexpr int kVarDirectShort = 1 << 11;  /* byte modes, keys <= 32 B: eight waves per CU, tiles in flight */
 constexpr int kVarDirectPairs = 1 << 10;  /* with kVarDirect8: the line image in rounds of two lines */
 static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash | kVarMd5PadTab | kVarDirectShort | kVarDirectPairs) &
@@ -2555,7 +2556,9 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
                                     ? (uint32_t)shape->min_len
                                     : 0u;
             return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream,
-                                  ((var >> 20) & 15) | ((var & kVarMd5PadTab) != 0 ? 16 : 0), fl);
+                                  ((var >> 20) & 15) | ((var & kVarMd5PadTab) != 0 ? 16 : 0) |
+                                      ((var & kVarMd5FullLines) != 0 ? 32 : 0),
+                                  fl);
         }
         const bool short_words = (var & kVarDirectShort) != 0 && nc_bytes::supports_short_words(mode) &&
                                  shape != nullptr && nkeys != 0 && shape->max_len <= 32u;

@@ -158,7 +158,7 @@ __device__ __forceinline__ void flush_tails(uint32_t *qmem, uint32_t (*qmeta)[2]
  * key i = keys[off[i], off[i+1]); keys stays readable NC_GPUHASH_PAD bytes
  * past off[nkeys]. A tile of 64 keys spans less than 4 GiB.
  */
-template <bool LDS, bool IL, int FL = 0, bool PT = false>
+template <bool LDS, bool IL, int FL = 0, bool PT = false, bool FS = false>
 __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
                                                            uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
@@ -295,10 +295,16 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                  * them here */
                 if constexpr (FIRST) md5_steps_first61(v, w);
                 else md5_steps(v, w, std::make_integer_sequence<int, 61>{});
-                if (fin) {
+                /* FS: a key whose last data block this is stores too, a
+                 * placeholder when its padding needs a tail block (run_tail
+                 * overwrites it): the tile's 256-byte store has no holes, so
+                 * HBM sees whole lines, not partial writes */
+                if (FS ? rem <= 64 : fin) {
                     const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
                     __builtin_amdgcn_raw_buffer_store_b32((FIRST ? NC_MD5_A0 : st[0]) + v[0], rout, (int)(lane * 4u),
                                                           0, kAuxNt);
+                }
+                if (fin) {
                 } else if (len - 56u > 8u) {
                     md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
                     st[0] = (FIRST ? NC_MD5_A0 : st[0]) + v[0];
@@ -343,7 +349,12 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                     q.w[8 * kQ + slot] = w[9];
                 }
                 q.count += (uint32_t)__builtin_popcountll(tm);
-                if (q.count >= 64u) run_tail(q, lane, out);
+                if (q.count >= 64u) {
+                    /* FS: this round's placeholders land before the tail
+                     * results that replace them */
+                    if constexpr (FS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    run_tail(q, lane, out);
+                }
             }
         }
 
@@ -476,7 +487,8 @@ void launch_fl(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uin
 
 /* var: bits 0-1 tiles per wave (0: 16, 1: 8, 2: 32, 3: 64); bit 2: the LDS-DMA
  * variant (long keys); bit 3 tiles interleaved over the grid; bit 4 the
- * padding selectors from the LDS table (pad_block_tab). fl: the batch's
+ * padding selectors from the LDS table (pad_block_tab); bit 5 whole-line
+ * stores (placeholders for the tail keys, FS). fl: the batch's
  * fixed key length if the caller's shape says so (0: unknown or varying);
  * 16, 20, 24, 32, 40 and 48 have specialised instantiations (each tile still
  * checks its lengths) */
@@ -510,6 +522,9 @@ hipError_t launch_pt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkey
         case 40: launch_fl<40, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
         default: launch_fl<48, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
         }
+    } else if (var & 32) {
+        hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, 0, PT, true>), dim3((unsigned)grid), dim3(256), 0,
+                           stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
     } else {
         hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, 0, PT>), dim3((unsigned)grid), dim3(256), 0, stream,
                            d_keys, d_off, nkeys, d_out, ntiles, chunk);
