@@ -1958,7 +1958,7 @@ constexpr int kVarDirect8 = 1 << 12;     /* line image: eight-wave workgroups, o
 constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
 constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
 constexpr int kVarMd5PadTab = 1 << 15;    /* md5: padding selectors from an LDS table */
-[[maybe_unused]] constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores */
+constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores */
 constexpr int kVarDirectShort = 1 << 11;  /* byte modes, keys <= 32 B: eight waves per CU, tiles in flight */
 constexpr int kVarDirectPairs = 1 << 10;  /* with kVarDirect8: the line image in rounds of two lines */
 static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash | kVarMd5PadTab | kVarDirectShort | kVarDirectPairs) &
@@ -2435,8 +2435,11 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
         /* ... and the per-lane padding selectors from the 512-byte LDS table
          * (pad_block_tab): C2 SQ_INSTS_VALU 443 M -> 408 M per launch,
          * 0.7319 -> 0.7259 and 0.7345 -> 0.7278 ms on two boxes
-         * (profiles/r05_md5_padtab_ab.jsonl, pmc_r05_md5pt.json) */
-        return kVarMd5Direct | (lds ? (12 << 20) : kVarMd5PadTab);
+         * (profiles/r05_md5_padtab_ab.jsonl, pmc_r05_md5pt.json); and
+         * whole-line output stores (the tail keys store a placeholder first,
+         * nc_md5_kernels.hip FS): C2 0.7333 -> 0.7048 ms, same box, same
+         * process (profiles/r06f_md5_fullline_ab.jsonl) */
+        return kVarMd5Direct | (lds ? (12 << 20) : kVarMd5PadTab | kVarMd5FullLines);
     }
     if (sh == nullptr || nkeys == 0 || sh->key_bytes == 0) return kVarRegStaged;
     const uint64_t mean = sh->key_bytes / nkeys;
