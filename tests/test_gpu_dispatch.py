@@ -230,10 +230,9 @@ def test_ketama_lookup_table(gpu, oracle, dist_fixture):
     16-bit ranges, 256 servers (the u8 server bytes' limit) on exactly 4,800
     points and 4,801 points (just past the LDS limit) and on 1,280 / 1,281
     (the packed LDS continuum's limit), points sharing their top 24 bits with
-    the keys' hashes (the packed search's full-value fallback), pools the
-    packed continuum's 1024-bucket index encodes and pools it leaves to the
-    u16[512] one (bit 18 forces that one), hash tags, against the oracle's
-    server_pool_idx."""
+    the keys' hashes (the packed search's full-value fallback), more packed
+    pools (skewed, tiny, few or ~128 servers), hash tags, against the
+    oracle's server_pool_idx."""
     import torch
 
     from twemproxy_amd import _lib as L
@@ -263,11 +262,9 @@ def test_ketama_lookup_table(gpu, oracle, dist_fixture):
         near += [h - 1, h, h + 1, (h & ~0xff) | rng.integers(0, 256, size=h.size), (h & ~0xff) | 0xff]
     near = np.unique(np.clip(np.concatenate(near), 0, (1 << 32) - 1)).astype(np.uint32)[:1280]
     pools.append((near, rng.integers(0, 200, size=near.size).astype(np.uint32), 200))
-    # the packed continuum's 1024-bucket index (round 6): pools it encodes
-    # (servers < 128: a direct bucket's byte is 128 + server; offsets from the
-    # 32-bucket anchors < 128) and pools it cannot, which keep the u16[512]
-    # index — a crowd of points in one bucket, a server >= 128 answering a
-    # direct bucket, points only in the top 1/256 of the ring, eight points
+    # more packed continua (<= 1,280 points): server counts around 128, points
+    # only in the top 1/256 of the ring, eight points, two servers, a crowd of
+    # 700 points in one 2^22 bucket
     for npts, nsrv, lo, hi in ((1280, 100, 0, 1 << 32), (1280, 128, 0, 1 << 32), (1280, 131, 0, 1 << 32),
                                (1200, 9, 0xff000000, 1 << 32), (8, 8, 0, 1 << 32), (1279, 2, 0, 1 << 32)):
         v = np.sort(rng.integers(lo, hi, size=npts, dtype=np.uint64)).astype(np.uint32)
@@ -284,9 +281,8 @@ def test_ketama_lookup_table(gpu, oracle, dist_fixture):
                     # grouped + 65536 / 4096 table in L2, grouped + bucket index over the L2 continuum,
                     # grouped + LDS continuum (256 / 512-key tiles), policy
                     # (bit 27: the 5-byte LDS continuum where the packed one fits)
-                    # (bit 18: the packed continuum's u16[512] index instead of the 1024-bucket one)
                     for var in ((1 << 30) | (1 << 24), (1 << 30) | (1 << 23), (1 << 30) | (1 << 25),
-                                (1 << 30) | (1 << 26), (1 << 30) | (1 << 27), (1 << 30) | (1 << 18), 1 << 30, 0):
+                                (1 << 30) | (1 << 26), (1 << 30) | (1 << 27), 1 << 30, 0):
                         L.lib().nc_gpuhash_set_tuning(0, 0, var)
                         got = t.server_idx_device(m, "ketama", kd, od, cd, nserver, hash_tag=tag, shape=shape)
                         torch.cuda.synchronize()
@@ -340,7 +336,7 @@ def test_ketama_packed_top_hashes(gpu, oracle):
         for vals, idx in pools:
             cd = t.continuum_device(idx, vals)
             want = oracle.server_idx_batch(6, 0, vals, idx, 8, None, pk, po)
-            for var in (0, 1 << 30, (1 << 30) | (1 << 27), (1 << 30) | (1 << 18)):
+            for var in (0, 1 << 30, (1 << 30) | (1 << 27)):
                 L.lib().nc_gpuhash_set_tuning(0, 0, var)
                 got = t.server_idx_device(6, "ketama", kd, od, cd, 8, shape=shape)
                 torch.cuda.synchronize()

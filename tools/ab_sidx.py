@@ -21,8 +21,6 @@ PIPES = {"policy": 0, "ring": 1 << 28, "workgroup": 1 << 29, "grouped": 1 << 30,
          # ketama pools of <= 1280 points: the packed LDS continuum (512-key tiles, 3 sets by default, or 8),
          # and the 5-byte one it replaces (bit 27)
          "grouped8": (1 << 30) | (3 << 21), "grouped_5b": (1 << 30) | (1 << 27),
-         # the packed continuum's round-5 u16[512] bucket index instead of the 1024-bucket one (bit 18)
-         "grouped_idx512": (1 << 30) | (1 << 18),
          # DIAGNOSTIC (fnv1a_64, packed continuum): no hash_tag code / no search (outputs are hashes) / neither
          "diag_notag": (1 << 30) | (1 << 19), "diag_nosearch": (1 << 30) | (2 << 19),
          "diag_bare": (1 << 30) | (3 << 19), "diag_bare_noprologue": (1 << 30) | (3 << 19) | (1 << 26),

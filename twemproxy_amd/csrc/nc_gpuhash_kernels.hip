@@ -274,9 +274,8 @@ __device__ __forceinline__ uint32_t ketama_find_lds(const uint32_t *vals, const 
  * finds the word's index and walks the run of such points comparing full
  * values from the continuum in global memory (cont: {server, value} pairs);
  * past the last point the answer wraps to point 0 (w0). */
-template <class Start>
-__device__ __forceinline__ uint32_t ketama_find_lds_packed_at(const uint32_t *w, Start start, const uint32_t *cont,
-                                                              uint32_t n, uint32_t w0, uint32_t h)
+__device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, const uint16_t *bkt16,
+                                                           const uint32_t *cont, uint32_t n, uint32_t w0, uint32_t h)
 {
     using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
     const uint32_t hb = h & ~0xffu; /* w >> 8 < h >> 8  <=>  w < hb */
@@ -285,7 +284,7 @@ __device__ __forceinline__ uint32_t ketama_find_lds_packed_at(const uint32_t *w,
      * unwritten; from at most n the search still ends at the sentinels (it
      * goes on only while a quad's last word is below hb, so it never reads
      * past word n + 3) */
-    uint32_t lo = min(start(), n) & ~3u;
+    uint32_t lo = min((uint32_t)bkt16[h >> 23], n) & ~3u;
     u32x4 a = q[lo >> 2];
     if (a.w < hb) { /* the quad's four words all below h: the next ones */
         do {
@@ -299,41 +298,12 @@ __device__ __forceinline__ uint32_t ketama_find_lds_packed_at(const uint32_t *w,
     if ((cand ^ hb) < 0x100u) { /* rare, the same top 24 bits: full values decide */
         /* from the bucket start again (re-read: keeping lo live past the
          * search loop makes hipcc carry derived addresses through it) */
-        uint32_t pos = min(start(), n) & ~3u;
+        uint32_t pos = min((uint32_t)bkt16[h >> 23], n) & ~3u;
         while (w[pos] < hb) pos++;
         while (pos < n && (w[pos] ^ hb) < 0x100u && cont[2u * pos + 1u] < h) pos++;
         cand = pos < n ? w[pos] : w0;
     }
     return cand & 0xffu;
-}
-
-__device__ __forceinline__ uint32_t ketama_find_lds_packed(const uint32_t *w, const uint16_t *bkt16,
-                                                           const uint32_t *cont, uint32_t n, uint32_t w0, uint32_t h)
-{
-    return ketama_find_lds_packed_at(w, [&]() { return (uint32_t)bkt16[h >> 23]; }, cont, n, w0, h);
-}
-
-/* Round 6: the same search behind a 1024-bucket index over the hash's top
- * 10 bits, one byte a bucket in the same 1 KiB (dt8), plus 32 u16 anchors
- * (anc16[k] = the first point of bucket 32k). A bucket that holds no point
- * (no packed word with those top 10 bits: ~29 % of buckets for 1280 points)
- * answers every hash in it with the next point's server, so its byte is
- * 128 + that server and the lane does no quad read; any other bucket's byte
- * is its first point's offset from its anchor (< 128). The two reads are
- * independent (the anchor table is 64 bytes: its reads broadcast), so a
- * searching lane still makes two dependent LDS round trips, as before, and a
- * quad read now has ~0.7 of the lanes: fewer bank conflicts, where the search
- * spends its time. Pools this cannot encode (a server index
- * >= 128 in a direct bucket, or an offset > 127) keep the u16[512] index:
- * the prologue decides per workgroup (ketama_idx1024_build). */
-__device__ __forceinline__ uint32_t ketama_find_lds_idx1024(const uint32_t *w, const uint8_t *dt8,
-                                                            const uint16_t *anc16, const uint32_t *cont, uint32_t n,
-                                                            uint32_t w0, uint32_t h)
-{
-    const uint32_t e = dt8[h >> 22];
-    const uint32_t a = anc16[h >> 27];
-    if (e >= 128u) return e - 128u;
-    return ketama_find_lds_packed_at(w, [&]() { return a + e; }, cont, n, w0, h);
 }
 
 /* lower bound of v over the continuum values (no wrap) */
@@ -781,10 +751,7 @@ struct GsLds {
     static constexpr uint32_t kNOff = D + 1;             /* offsets of tiles t .. t+D */
     static constexpr uint32_t kPermBytes = 2u * 2u * TK; /* u16[2][TK]: sorted position -> key index */
     static constexpr uint32_t kResBytes = CS ? 2u * 4u * TK : 0u; /* u32[2][TK]: hashes by key index */
-    /* RSV (the packed ketama continuum): u16[32] bucket anchors and the
-     * index form's flag word (ketama_find_lds_idx1024) */
-    static constexpr uint32_t kAncBytes = RSV > 0 ? 80u : 0u;
-    static constexpr uint32_t kFixed = kNOff * kOffSlot + kPermBytes + 4 * 64 + 4 * 256 + 16 + kResBytes + kAncBytes;
+    static constexpr uint32_t kFixed = kNOff * kOffSlot + kPermBytes + 4 * 64 + 4 * 256 + 16 + kResBytes;
     /* 8 / 7 workgroups of four waves per CU; 4 of eight (1024-key tiles of
      * sixteen waves, two per CU, measured 40 % slower) */
     /* RSV: bytes left to dynamic LDS (a packed ketama continuum) within the
@@ -797,8 +764,7 @@ struct GsLds {
     static constexpr uint32_t kTab = kHist + 4 * 64;            /* u32[256]: crc table / ketama bucket index */
     static constexpr uint32_t kDump = kTab + 4 * 256;           /* landing area of dummy DMAs */
     static constexpr uint32_t kRes = kDump + 16;
-    static constexpr uint32_t kAnc = kRes + kResBytes;
-    static constexpr uint32_t kBytes = kAnc + kAncBytes;
+    static constexpr uint32_t kBytes = kRes + kResBytes;
     static constexpr int kSlabIters = (int)((kCap / 16 + TK - 1) / TK);
     static_assert(kBytes <= kBudget, "LDS budget");
     static_assert(kOffs % 16 == 0 && kTab % 16 == 0 && kCap % 16 == 0 && kRes % 16 == 0,
@@ -989,10 +955,6 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
     uint32_t pad_src = 0u; /* md5: the padding perms' constant in a VGPR (a uniform selector takes the SGPR slot) */
     if constexpr (MODE == NC_GPUHASH_MD5) asm volatile("v_mov_b32 %0, %1" : "=v"(pad_src) : "i"(nc_md5s::kPadSrc));
     uint32_t pw0 = 0u; /* the packed continuum's first word */
-    /* packed continuum: the 1024-bucket index (round 6) unless VAR bit 10
-     * (A/B: the u16[512] index) or a pool it cannot encode */
-    constexpr bool kOldIdx = (VAR & 1024) != 0;
-    bool idx1024 = false;
     if (t < 256u) {
         if constexpr (uses_crc_table<MODE>())
             tab[t] = (MODE == NC_GPUHASH_CRC16) ? nc_crc16_entry(t) : nc_crc32_entry(t);
@@ -1027,61 +989,14 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
          * starts the buckets after its predecessor's up to its own, the last
          * point ends the rest at n */
         __syncthreads();
+        uint16_t *bkt16 = reinterpret_cast<uint16_t *>(tab);
         const uint32_t n = dist.ncont;
-        bool old_idx = kOldIdx;
-        if constexpr (!kOldIdx) {
-            /* the 1024-bucket form (ketama_find_lds_idx1024): bucket b's
-             * first point p(b) (the first word whose top 10 bits are >= b;
-             * n, the first sentinel, if none) by a binary search over the
-             * staged words, its anchor p(b & ~31) likewise */
-            uint8_t *dt8 = reinterpret_cast<uint8_t *>(tab);
-            uint16_t *anc16 = reinterpret_cast<uint16_t *>(smem + G::kAnc);
-            uint32_t *flag = reinterpret_cast<uint32_t *>(smem + G::kAnc + 64u);
-            if (t == 0u) *flag = 0u;
-            __syncthreads();
-            auto first_at = [&](uint32_t b) {
-                uint32_t lo = 0u, cnt = n;
-                while (cnt > 0u) {
-                    const uint32_t half = cnt >> 1;
-                    if ((gs_cont[lo + half] >> 22) < b) {
-                        lo += half + 1u;
-                        cnt -= half + 1u;
-                    } else {
-                        cnt = half;
-                    }
-                }
-                return lo;
-            };
-            bool bad = false;
-            for (uint32_t b = t; b < 1024u; b += TK) {
-                const uint32_t p = first_at(b), a = first_at(b & ~31u), wp = gs_cont[p];
-                uint32_t e;
-                if ((wp >> 22) != b) { /* no point in the bucket: the next point's server answers all of it */
-                    e = 128u + (wp & 0xffu);
-                    bad |= (wp & 0xffu) >= 128u;
-                } else {
-                    e = p - a;
-                    bad |= e >= 128u;
-                }
-                dt8[b] = (uint8_t)e;
-                if ((b & 31u) == 0u) anc16[b >> 5] = (uint16_t)p;
-            }
-            if (bad) __hip_atomic_fetch_or(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __syncthreads();
-            old_idx = __builtin_amdgcn_readfirstlane((int)*flag) != 0;
-            if (old_idx) __syncthreads(); /* (uniform) every read of dt8 is done before the u16 form overwrites it */
+        for (uint32_t i = t; i < n; i += TK) {
+            const uint32_t cb = gs_cont[i] >> 23;
+            for (uint32_t bb = i == 0u ? 0u : (gs_cont[i - 1u] >> 23) + 1u; bb <= cb; bb++) bkt16[bb] = (uint16_t)i;
+            if (i == n - 1u)
+                for (uint32_t bb = cb + 1u; bb < 512u; bb++) bkt16[bb] = (uint16_t)n;
         }
-        if (old_idx) {
-            uint16_t *bkt16 = reinterpret_cast<uint16_t *>(tab);
-            for (uint32_t i = t; i < n; i += TK) {
-                const uint32_t cb = gs_cont[i] >> 23;
-                for (uint32_t bb = i == 0u ? 0u : (gs_cont[i - 1u] >> 23) + 1u; bb <= cb; bb++)
-                    bkt16[bb] = (uint16_t)i;
-                if (i == n - 1u)
-                    for (uint32_t bb = cb + 1u; bb < 512u; bb++) bkt16[bb] = (uint16_t)n;
-            }
-        }
-        idx1024 = !old_idx;
     }
 
     /* prologue: offsets of tiles 0 .. D-1; perm(0); slabs 0 .. D-2 */
@@ -1192,15 +1107,9 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
             if constexpr (wg_dist<VAR>() == kDistKetamaLds)
                 h = ketama_find_lds(gs_cont, reinterpret_cast<const uint8_t *>(gs_cont + dist.ncont), tab, dist.ncont,
                                     h);
-            else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked && (VAR & 128) == 0) { /* bit 7: DIAGNOSTIC */
-                if (!kOldIdx && idx1024)
-                    h = ketama_find_lds_idx1024(gs_cont, reinterpret_cast<const uint8_t *>(tab),
-                                                reinterpret_cast<const uint16_t *>(smem + G::kAnc), dist.cont,
-                                                dist.ncont, pw0, h);
-                else
-                    h = ketama_find_lds_packed(gs_cont, reinterpret_cast<const uint16_t *>(tab), dist.cont,
-                                               dist.ncont, pw0, h);
-            }
+            else if constexpr (wg_dist<VAR>() == kDistKetamaLdsPacked && (VAR & 128) == 0) /* bit 7: DIAGNOSTIC */
+                h = ketama_find_lds_packed(gs_cont, reinterpret_cast<const uint16_t *>(tab), dist.cont, dist.ncont,
+                                           pw0, h);
 
             if constexpr (CS) {
                 gs_ds_write_b32(lds_base + G::kRes + (it & 1u) * 4u * TK + 4u * i, h);
@@ -2043,14 +1952,15 @@ constexpr uint32_t kLdsContMax = 4800; /* ketama points the grouped pipeline sta
 constexpr uint32_t kLdsPackedMax = 1280; /* ... packed, 4 B each (+ 8 sentinels), beside four 512-key
                                             workgroups per CU */
 constexpr int kVarNoPacked = 1 << 27; /* server_idx A/B: the 5-byte LDS continuum even where the packed one fits */
-constexpr int kVarKetamaIdx512 = 1 << 18; /* server_idx A/B: the packed continuum's u16[512] index (round 5) */
 /* direct byte kernels' options beyond bits 20-23, in bits only the ring
  * pipeline reads otherwise (bit 19 selects the direct pipeline first) */
 constexpr int kVarDirect8 = 1 << 12;     /* line image: eight-wave workgroups, one per CU */
 constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
 constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
 constexpr int kVarMd5PadTab = 1 << 15;    /* md5: padding selectors from an LDS table */
-constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores */
+constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores; with it
+                                             bits 13 / 14 (the byte kernels' S8 / NoHash) are A/B store
+                                             policies (nc_md5_kernels.hip SP) */
 constexpr int kVarDirectShort = 1 << 11;  /* byte modes, keys <= 32 B: eight waves per CU, tiles in flight */
 constexpr int kVarDirectPairs = 1 << 10;  /* with kVarDirect8: the line image in rounds of two lines */
 static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash | kVarMd5PadTab | kVarDirectShort | kVarDirectPairs) &
@@ -2471,9 +2381,6 @@ hipError_t nc_tu::entry_dist(const uint8_t *base, const uint64_t *off, uint64_t 
                         default: break;
                         }
                     }
-                    if (d.gs_var & kVarKetamaIdx512) /* A/B: the round-5 u16[512] bucket index */
-                        return launch_gs<MODE, (5 << 12) | 1024, 2, true, 512, kR>(base, off, delta, nkeys, out,
-                                                                                   stream, sets, wd, dyn);
                     return launch_gs<MODE, 5 << 12, 2, true, 512, kR>(base, off, delta, nkeys, out, stream, sets, wd,
                                                                        dyn);
                 }
@@ -2655,7 +2562,8 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
                                     : 0u;
             return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream,
                                   ((var >> 20) & 15) | ((var & kVarMd5PadTab) != 0 ? 16 : 0) |
-                                      ((var & kVarMd5FullLines) != 0 ? 32 : 0),
+                                      ((var & kVarMd5FullLines) != 0 ? 32 : 0) |
+                                      ((var & kVarDirectS8) != 0 ? 64 : 0) | ((var & kVarDirectNoHash) != 0 ? 128 : 0),
                                   fl);
         }
         const bool short_words = (var & kVarDirectShort) != 0 && nc_bytes::supports_short_words(mode) &&
@@ -2801,8 +2709,7 @@ extern "C" rstatus_t nc_gpuhash_server_idx_device(int mode, int dist, const uint
     if (tuned & (1 << 29)) wg = true;
     if (tuned & (1 << 28)) wg = false;
     nc_tu::DistArgs d{reinterpret_cast<const uint32_t *>(d_continuum), ncontinuum, 0u, dist, wide, wg, gs,
-                      tuned & ((3 << 19) | (3 << 21) | (1 << 26) | kVarNoPacked | kVarKetamaIdx512), nullptr, 20u,
-                      gs && lds_cont};
+                      tuned & ((3 << 19) | (3 << 21) | (1 << 26) | kVarNoPacked), nullptr, 20u, gs && lds_cont};
     if (hash_tag != nullptr)
         d.tag = (uint32_t)(uint8_t)hash_tag[0] | ((uint32_t)(uint8_t)hash_tag[1] << 8) | (1u << 16);
     /* A/B only: ketama on the workgroup pipelines through a lookup table
