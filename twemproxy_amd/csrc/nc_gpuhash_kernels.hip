@@ -1958,9 +1958,7 @@ constexpr int kVarDirect8 = 1 << 12;     /* line image: eight-wave workgroups, o
 constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
 constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
 constexpr int kVarMd5PadTab = 1 << 15;    /* md5: padding selectors from an LDS table */
-constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores; with it
-                                             bits 13 / 14 (the byte kernels' S8 / NoHash) are A/B store
-                                             policies (nc_md5_kernels.hip SP) */
+constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores */
 constexpr int kVarDirectShort = 1 << 11;  /* byte modes, keys <= 32 B: eight waves per CU, tiles in flight */
 constexpr int kVarDirectPairs = 1 << 10;  /* with kVarDirect8: the line image in rounds of two lines */
 static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash | kVarMd5PadTab | kVarDirectShort | kVarDirectPairs) &
@@ -2562,8 +2560,7 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
                                     : 0u;
             return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream,
                                   ((var >> 20) & 15) | ((var & kVarMd5PadTab) != 0 ? 16 : 0) |
-                                      ((var & kVarMd5FullLines) != 0 ? 32 : 0) |
-                                      ((var & kVarDirectS8) != 0 ? 64 : 0) | ((var & kVarDirectNoHash) != 0 ? 128 : 0),
+                                      ((var & kVarMd5FullLines) != 0 ? 32 : 0),
                                   fl);
         }
         const bool short_words = (var & kVarDirectShort) != 0 && nc_bytes::supports_short_words(mode) &&

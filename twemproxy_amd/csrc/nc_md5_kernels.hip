@@ -82,7 +82,6 @@ __device__ __forceinline__ uint32_t lanemask_lt_popc(uint64_t m)
  * (message words 11, 2, 9) and the state add finish here, 64 lanes at a
  * time, instead of in every round a wave holds such a key. Any other queued
  * key (empty, or longer than 64 bytes) carries its chaining state in X. */
-template <bool TNT = true>
 __device__ __forceinline__ void tail_entry(const uint32_t *qw, uint32_t slot, uint32_t *__restrict__ out)
 {
     uint32_t st[4] = {qw[0 * kQ + slot], qw[1 * kQ + slot], qw[2 * kQ + slot], qw[3 * kQ + slot]};
@@ -103,15 +102,13 @@ __device__ __forceinline__ void tail_entry(const uint32_t *qw, uint32_t slot, ui
     w[14] = len << 3;
     w[15] = len >> 29;
     /* words 1..13 are zero: folded into the steps' constants */
-    if constexpr (TNT) __builtin_nontemporal_store(md5_tail_final_a(st, w), out + idx);
-    else out[idx] = md5_tail_final_a(st, w);
+    __builtin_nontemporal_store(md5_tail_final_a(st, w), out + idx);
 }
 
-template <bool TNT = true>
 __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__restrict__ out)
 {
     const uint32_t n = q.count < 64u ? q.count : 64u;
-    if (lane < n) tail_entry<TNT>(q.w, (q.head + lane) & (kQ - 1u), out);
+    if (lane < n) tail_entry(q.w, (q.head + lane) & (kQ - 1u), out);
     q.head = (q.head + n) & (kQ - 1u);
     q.count -= n;
 }
@@ -120,7 +117,6 @@ __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__re
  * from the concatenation of the waves' queues goes to wave k mod kWaves
  * (one partly filled tail round per wave would cost each wave a full round
  * of steps for its last few keys). Every wave of the workgroup calls it. */
-template <bool TNT = true>
 __device__ __forceinline__ void flush_tails(uint32_t *qmem, uint32_t (*qmeta)[2], const Queue &q, uint32_t wave,
                                             uint32_t lane, uint32_t *__restrict__ out)
 {
@@ -148,7 +144,7 @@ __device__ __forceinline__ void flush_tails(uint32_t *qmem, uint32_t (*qmeta)[2]
                 h = sw == i ? head[i] : h;
                 p = sw == i ? pre[i] : p;
             }
-            tail_entry<TNT>(qmem + sw * kQWords * kQ, (h + e - p) & (kQ - 1u), out);
+            tail_entry(qmem + sw * kQWords * kQ, (h + e - p) & (kQ - 1u), out);
         }
     }
 }
@@ -162,11 +158,7 @@ __device__ __forceinline__ void flush_tails(uint32_t *qmem, uint32_t (*qmeta)[2]
  * key i = keys[off[i], off[i+1]); keys stays readable NC_GPUHASH_PAD bytes
  * past off[nkeys]. A tile of 64 keys spans less than 4 GiB.
  */
-/* SP (A/B, with FS): 0 every output store non-temporal; 1 the tiles'
- * stores with the default policy (their lines stay in L2 / the Infinity
- * Cache, where a tail key's later 4-byte store can merge); 2 the tail stores
- * too */
-template <bool LDS, bool IL, int FL = 0, bool PT = false, bool FS = false, int SP = 0>
+template <bool LDS, bool IL, int FL = 0, bool PT = false, bool FS = false>
 __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
                                                            uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
@@ -310,7 +302,7 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                 if (FS ? rem <= 64 : fin) {
                     const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
                     __builtin_amdgcn_raw_buffer_store_b32((FIRST ? NC_MD5_A0 : st[0]) + v[0], rout, (int)(lane * 4u),
-                                                          0, SP >= 1 ? 0 : kAuxNt);
+                                                          0, kAuxNt);
                 }
                 if (fin) {
                 } else if (len - 56u > 8u) {
@@ -361,7 +353,7 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                     /* FS: this round's placeholders land before the tail
                      * results that replace them */
                     if constexpr (FS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    run_tail<SP < 2>(q, lane, out);
+                    run_tail(q, lane, out);
                 }
             }
         }
@@ -384,7 +376,7 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
     }
     /* (pooled for the generic kernel; the fixed-length instantiations queue
      * almost nothing, and the pooled flush there made hipcc spill) */
-    if constexpr (FL == 0) flush_tails<SP < 2>(qmem, qmeta, q, wave, lane, out);
+    if constexpr (FL == 0) flush_tails(qmem, qmeta, q, wave, lane, out);
     else while (q.count != 0u) run_tail(q, lane, out);
 }
 
@@ -496,8 +488,7 @@ void launch_fl(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uin
 /* var: bits 0-1 tiles per wave (0: 16, 1: 8, 2: 32, 3: 64); bit 2: the LDS-DMA
  * variant (long keys); bit 3 tiles interleaved over the grid; bit 4 the
  * padding selectors from the LDS table (pad_block_tab); bit 5 whole-line
- * stores (placeholders for the tail keys, FS); with it, A/B bits 6 / 7: the
- * store policy SP 1 / 2. fl: the batch's
+ * stores (placeholders for the tail keys, FS). fl: the batch's
  * fixed key length if the caller's shape says so (0: unknown or varying);
  * 16, 20, 24, 32, 40 and 48 have specialised instantiations (each tile still
  * checks its lengths) */
@@ -532,15 +523,8 @@ hipError_t launch_pt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkey
         default: launch_fl<48, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
         }
     } else if (var & 32) {
-        if (var & 64)
-            hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, 0, PT, true, 1>), dim3((unsigned)grid), dim3(256), 0,
-                               stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
-        else if (var & 128)
-            hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, 0, PT, true, 2>), dim3((unsigned)grid), dim3(256), 0,
-                               stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
-        else
-            hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, 0, PT, true>), dim3((unsigned)grid), dim3(256), 0,
-                               stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
+        hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, 0, PT, true>), dim3((unsigned)grid), dim3(256), 0,
+                           stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
     } else {
         hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, 0, PT>), dim3((unsigned)grid), dim3(256), 0, stream,
                            d_keys, d_off, nkeys, d_out, ntiles, chunk);
