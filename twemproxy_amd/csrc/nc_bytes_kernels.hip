@@ -87,6 +87,7 @@ constexpr uint32_t kTabWords = nc_slice::table_words<kCopies>();
 constexpr int kOptS8 = 1;     /* slicing-by-8 crcs */
 constexpr int kOptNoHash = 2; /* DIAGNOSTIC: xor of the key's words, not a hash (the pipeline's memory side) */
 constexpr int kOptPairs = 16; /* the line image's rounds of two lines (256 B per key; eight-wave workgroups) */
+constexpr int kOptOffDefault = 32; /* A/B: the offsets with the default cache policy instead of nt */
 
 template <int MODE, bool LDS, int OPT>
 struct Tab {
@@ -213,8 +214,9 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
     wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + (LDS ? wave * kImg : 0u);
 
-    TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
-    Offs no = wk.load_off(tile + 1u);
+    constexpr int kOffAux = (OPT & kOptOffDefault) != 0 ? 0 : kAuxNt;
+    TileKeys cur_t = wk.keys_of(tile, wk.template load_off<kOffAux>(tile));
+    Offs no = wk.template load_off<kOffAux>(tile + 1u);
     u32x4 da[4], db[4];
     if constexpr (PAIRS) wk.dma_pairs(cur_t, 0u, img);
     else if constexpr (LDS) wk.dma_lines(cur_t, 0u, img);
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
         }
         /* offsets two tiles ahead, straight into `no` (it was consumed above);
          * a re-read of the next tile's while this one still has blocks */
-        no = wk.load_off(more ? tile + 1u : tile + 2u);
+        no = wk.template load_off<kOffAux>(more ? tile + 1u : tile + 2u);
 
         const int32_t rem = (int32_t)cur_t.len - (int32_t)RB * (int32_t)b;
         if (cur_t.valid && (rem > 0 || (b == 0u && cur_t.len == 0u))) {
@@ -687,6 +689,7 @@ hipError_t launch_mode(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nk
     } else {
     if constexpr (MODE == NC_GPUHASH_FNV1A_64 || MODE == NC_GPUHASH_CRC32) {
         if (var & 64) return launch_opt<MODE, kOptNoHash>(d_keys, d_off, nkeys, d_out, stream, var);
+        if (var & 512) return launch_opt<MODE, kOptOffDefault>(d_keys, d_off, nkeys, d_out, stream, var);
     }
     if constexpr (has_table<MODE>()) {
         if (var & 32) return launch_opt<MODE, kOptS8>(d_keys, d_off, nkeys, d_out, stream, var);

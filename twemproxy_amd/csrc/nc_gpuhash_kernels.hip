@@ -1958,9 +1958,12 @@ constexpr int kVarDirect8 = 1 << 12;     /* line image: eight-wave workgroups, o
 constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
 constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
 constexpr int kVarMd5PadTab = 1 << 15;    /* md5: padding selectors from an LDS table */
-constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores */
+constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores; bit 13
+                                             (the crcs' S8) A/B: the line kernel's offsets, default policy */
 constexpr int kVarDirectShort = 1 << 11;  /* byte modes, keys <= 32 B: eight waves per CU, tiles in flight */
 constexpr int kVarDirectPairs = 1 << 10;  /* with kVarDirect8: the line image in rounds of two lines */
+constexpr int kVarDirectOffDefault = 1 << 9; /* A/B (crc32, fnv1a_64): the offsets with the default cache policy
+                                                (bits 8-9 are ring options, unread on the direct path) */
 static_assert(((kVarDirect8 | kVarDirectS8 | kVarDirectNoHash | kVarMd5PadTab | kVarDirectShort | kVarDirectPairs) &
                (kVarMd5Direct | (15 << 20) | kVarNoFixedLen | kVarWsort | kVarGsort | kVarNoPacked | (3 << 29))) == 0,
               "direct-pipeline options overlap the pipeline choice, its nibble or the server_idx bits");
@@ -2496,6 +2499,11 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
      * r05b_modes_c3.json, and keeps it) */
     if (fixed && mean >= 20u && sh->max_len <= 32u && mode == NC_GPUHASH_CRC16)
         return kVarDirect | kVarDirectShort | kVarDirect8;
+    /* ... and jenkins (round 6): 0.5974 -> 0.5858 ms against its
+     * register-staged pipeline, same process; one to three tiles in flight
+     * within 0.4 % (profiles/r06j_c3_jenkins_short16_ab.jsonl) */
+    if (fixed && mean >= 20u && sh->max_len <= 32u && mode == NC_GPUHASH_JENKINS)
+        return kVarDirect | kVarDirectShort | kVarDirect8;
     /* fixed-length short keys: the crcs' slicing-by-4 tables on the direct
      * pipeline (C3: 0.70 -> 0.61 ms); varying lengths keep the length-grouped
      * workgroup pipelines (a direct wave runs to its longest key) */
@@ -2560,7 +2568,8 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
                                     : 0u;
             return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream,
                                   ((var >> 20) & 15) | ((var & kVarMd5PadTab) != 0 ? 16 : 0) |
-                                      ((var & kVarMd5FullLines) != 0 ? 32 : 0),
+                                      ((var & kVarMd5FullLines) != 0 ? 32 : 0) |
+                                      ((var & kVarDirectS8) != 0 ? 64 : 0),
                                   fl);
         }
         const bool short_words = (var & kVarDirectShort) != 0 && nc_bytes::supports_short_words(mode) &&
@@ -2569,7 +2578,8 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
             return nc_bytes::launch(mode, d_keys, d_off, nkeys, d_out, stream,
                                     ((var >> 20) & 15) | ((var & kVarDirect8) != 0 ? 16 : 0) |
                                         ((var & kVarDirectS8) != 0 ? 32 : 0) | ((var & kVarDirectNoHash) != 0 ? 64 : 0) |
-                                        ((var & kVarDirectShort) != 0 ? 128 : 0) | ((var & kVarDirectPairs) != 0 ? 256 : 0),
+                                        ((var & kVarDirectShort) != 0 ? 128 : 0) | ((var & kVarDirectPairs) != 0 ? 256 : 0) |
+                                        ((var & kVarDirectOffDefault) != 0 ? 512 : 0),
                                     shape != nullptr && nkeys != 0 ? (uint32_t)shape->max_len : 0xffffffffu);
     }
     if ((var & kVarWsort) != 0 && nkeys < (1ull << 32) && nc_wsort::supports(mode))

@@ -388,7 +388,10 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
  * (with long keys every lane of a tile usually needs it at once, so there is
  * no queue).
  */
-template <bool IL>
+/* OA: the offsets' cache policy (A/B: nt, the byte kernels', or the
+ * default, which the direct kernel takes: a lane's start and end dwords
+ * share lines that nt can evict between the two loads) */
+template <bool IL, int OA = kAuxNt>
 __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
                                                            uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
@@ -403,8 +406,8 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
     Walker<IL> wk;
     wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + wave * kLineImage;
-    TileKeys cur_t = wk.keys_of(tile, wk.load_off(tile));
-    Offs no = wk.load_off(tile + 1u);
+    TileKeys cur_t = wk.keys_of(tile, wk.template load_off<OA>(tile));
+    Offs no = wk.template load_off<OA>(tile + 1u);
     wk.dma_lines(cur_t, 0u, img);
     uint32_t b = 0;
     uint32_t st[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
@@ -442,7 +445,7 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
         wk.read_lines(img, d0, d1);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the image's reads are done */
         wk.dma_lines(more ? cur_t : nxt_t, more ? b + 1u : 0u, img);
-        no = wk.load_off(more ? tile + 1u : tile + 2u);
+        no = wk.template load_off<OA>(more ? tile + 1u : tile + 2u);
 
         const int32_t rem = (int32_t)cur_t.len - 128 * (int32_t)b; /* key bytes from this line's start */
         if (cur_t.valid && rem > 0) block(d0, rem);
@@ -488,7 +491,8 @@ void launch_fl(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uin
 /* var: bits 0-1 tiles per wave (0: 16, 1: 8, 2: 32, 3: 64); bit 2: the LDS-DMA
  * variant (long keys); bit 3 tiles interleaved over the grid; bit 4 the
  * padding selectors from the LDS table (pad_block_tab); bit 5 whole-line
- * stores (placeholders for the tail keys, FS). fl: the batch's
+ * stores (placeholders for the tail keys, FS); bit 6 (A/B) the line kernel's
+ * offsets with the default cache policy (OA). fl: the batch's
  * fixed key length if the caller's shape says so (0: unknown or varying);
  * 16, 20, 24, 32, 40 and 48 have specialised instantiations (each tile still
  * checks its lengths) */
@@ -504,7 +508,10 @@ hipError_t launch_pt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkey
     (void)hipGetLastError();
     const bool il = (var & 8) != 0;
     if (var & 4) {
-        if (il)
+        if (il && (var & 64))
+            hipLaunchKernelGGL((nc_md5_lines_kernel<true, 0>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
+                               d_off, nkeys, d_out, ntiles, chunk);
+        else if (il)
             hipLaunchKernelGGL(nc_md5_lines_kernel<true>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off,
                                nkeys, d_out, ntiles, chunk);
         else
