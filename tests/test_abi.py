@@ -149,7 +149,8 @@ def test_auto_policy_choices():
     n = 1 << 26
     assert t.pick_variant("fnv1a_64", n) == RS
     PADTAB = 1 << 15  # md5: padding selectors from the LDS table
-    assert t.pick_variant("md5", n) == DIRECT | PADTAB  # unknown shape
+    FULL = 1 << 12  # md5: whole-line output stores (round 6)
+    assert t.pick_variant("md5", n) == DIRECT | PADTAB | FULL  # unknown shape
     # C2 (Zipf 8-64 B, mean 19.3)
     for name in ("fnv1a_64", "fnv1_64", "fnv1_32", "fnv1a_32"):  # six resident sets
         assert t.pick_variant(name, n, (19 * n, 8, 64)) == GSORT | CS | TK512, name
@@ -159,17 +160,17 @@ def test_auto_policy_choices():
     assert t.pick_variant("crc32", n, (19 * n, 8, 64)) == WG | OVER
     assert t.pick_variant("one_at_a_time", n, (19 * n, 8, 64)) == GSORT | CS | TK512 | ISSUE
     assert t.pick_variant("one_at_a_time", n, (21 * n, 8, 64)) == GSORT | CS | TK512 | ISSUE
-    assert t.pick_variant("md5", n, (19 * n, 8, 64)) == DIRECT | PADTAB
+    assert t.pick_variant("md5", n, (19 * n, 8, 64)) == DIRECT | PADTAB | FULL
     # uniform 8-64 B (mean 36)
     assert t.pick_variant("fnv1a_64", n, (36 * n, 8, 64)) == RS
-    assert t.pick_variant("md5", n, (36 * n, 8, 64)) == DIRECT | PADTAB
+    assert t.pick_variant("md5", n, (36 * n, 8, 64)) == DIRECT | PADTAB | FULL
     assert t.pick_variant("crc32a", n, (36 * n, 8, 64)) == RS | OVER
     # C3 (fixed 32 B)
     for name in ("fnv1_64", "fnv1a_64", "fnv1_32", "fnv1a_32", "hsieh"):
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == RING5, name
     SHORT = 1 << 11  # the short-key kernel (eight waves per CU); bits 20-21 depth, 22-23 the crc tables
     assert t.pick_variant("crc16", n, (32 * n, 32, 32)) == DIRECT | SHORT | (1 << 12)  # sixteen waves per CU
-    assert t.pick_variant("jenkins", n, (32 * n, 32, 32)) == RS
+    assert t.pick_variant("jenkins", n, (32 * n, 32, 32)) == DIRECT | SHORT | (1 << 12)  # sixteen waves (round 6)
     for name in ("crc32", "crc32a"):  # three tiles in flight, slicing-by-8
         assert t.pick_variant(name, n, (32 * n, 32, 32)) == DIRECT | SHORT | (2 << 20) | (1 << 22), name
     assert t.pick_variant("one_at_a_time", n, (32 * n, 32, 32)) == DIRECT | SHORT | (2 << 20)
@@ -177,10 +178,10 @@ def test_auto_policy_choices():
     assert t.pick_variant("murmur", n, (36 * n, 36, 36)) == RING5  # longer than 32 B
     assert t.pick_variant("crc32", n, (36 * n, 36, 36)) == DIRECT | IL32  # longer than 32 B
     assert t.pick_variant("jenkins", n, (36 * n, 36, 36)) == RS
-    assert t.pick_variant("md5", n, (32 * n, 32, 32)) == DIRECT | PADTAB
+    assert t.pick_variant("md5", n, (32 * n, 32, 32)) == DIRECT | PADTAB | FULL
     # short fixed, long keys (C4)
     assert t.pick_variant("fnv1a_64", n, (8 * n, 8, 8)) == WG
-    assert t.pick_variant("md5", n, (16 * n, 16, 16)) == DIRECT | PADTAB
+    assert t.pick_variant("md5", n, (16 * n, 16, 16)) == DIRECT | PADTAB | FULL
     for name in ("crc32", "one_at_a_time", "crc16"):
         assert t.pick_variant(name, n >> 3, (256 * (n >> 3), 256, 256)) == DIRECT | DIRECT_LDS | IL32, name
     for name in ("fnv1a_64", "fnv1_32"):  # eight-wave workgroups, one per CU, rounds of two lines
