@@ -214,7 +214,12 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
     wk.init(keys, off, nkeys, tiles, lane);
     uint8_t *const img = kbuf + (LDS ? wave * kImg : 0u);
 
-    constexpr int kOffAux = (OPT & kOptOffDefault) != 0 ? 0 : kAuxNt;
+    /* the offsets' cache policy: the default for the crcs' line image (a
+     * lane's start and end dwords share lines nt can evict between the two
+     * loads: C4 shard crc32 1.7965 -> 1.7758 ms, HBM reads 9.32 -> 9.16 GB,
+     * profiles/r06k_c4_offsets_policy_ab_crc32.jsonl), nt elsewhere (the
+     * fnvs' line kernel ties, 1.5361 vs 1.5391; A/B: kOptOffDefault) */
+    constexpr int kOffAux = ((OPT & kOptOffDefault) != 0 || (LDS && has_table<MODE>())) ? 0 : kAuxNt;
     TileKeys cur_t = wk.keys_of(tile, wk.template load_off<kOffAux>(tile));
     Offs no = wk.template load_off<kOffAux>(tile + 1u);
     u32x4 da[4], db[4];

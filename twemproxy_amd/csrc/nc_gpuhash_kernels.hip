@@ -1959,7 +1959,7 @@ constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
 constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
 constexpr int kVarMd5PadTab = 1 << 15;    /* md5: padding selectors from an LDS table */
 constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores; bit 13
-                                             (the crcs' S8) A/B: the line kernel's offsets, default policy */
+                                             (the crcs' S8) A/B: the line kernel's offsets non-temporal */
 constexpr int kVarDirectShort = 1 << 11;  /* byte modes, keys <= 32 B: eight waves per CU, tiles in flight */
 constexpr int kVarDirectPairs = 1 << 10;  /* with kVarDirect8: the line image in rounds of two lines */
 constexpr int kVarDirectOffDefault = 1 << 9; /* A/B (crc32, fnv1a_64): the offsets with the default cache policy

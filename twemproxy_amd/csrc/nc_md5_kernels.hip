@@ -388,10 +388,12 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
  * (with long keys every lane of a tile usually needs it at once, so there is
  * no queue).
  */
-/* OA: the offsets' cache policy (A/B: nt, the byte kernels', or the
- * default, which the direct kernel takes: a lane's start and end dwords
- * share lines that nt can evict between the two loads) */
-template <bool IL, int OA = kAuxNt>
+/* OA: the offsets' cache policy — the default, as the direct kernel's: a
+ * lane's start and end dwords share lines that nt can evict between the two
+ * loads (C4 shard 1.8063 -> 1.7884 ms, HBM reads 9.48 -> 9.29 GB per launch,
+ * profiles/r06k_c4_offsets_policy_ab_md5.jsonl, pmc_r06k_c4_offsets_policy.json);
+ * nt (kAuxNt, the round-5 form) by A/B bit 6 */
+template <bool IL, int OA = 0>
 __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
                                                            uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
@@ -492,7 +494,7 @@ void launch_fl(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uin
  * variant (long keys); bit 3 tiles interleaved over the grid; bit 4 the
  * padding selectors from the LDS table (pad_block_tab); bit 5 whole-line
  * stores (placeholders for the tail keys, FS); bit 6 (A/B) the line kernel's
- * offsets with the default cache policy (OA). fl: the batch's
+ * offsets non-temporal (OA, the round-5 form). fl: the batch's
  * fixed key length if the caller's shape says so (0: unknown or varying);
  * 16, 20, 24, 32, 40 and 48 have specialised instantiations (each tile still
  * checks its lengths) */
@@ -509,8 +511,8 @@ hipError_t launch_pt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkey
     const bool il = (var & 8) != 0;
     if (var & 4) {
         if (il && (var & 64))
-            hipLaunchKernelGGL((nc_md5_lines_kernel<true, 0>), dim3((unsigned)grid), dim3(256), 0, stream, d_keys,
-                               d_off, nkeys, d_out, ntiles, chunk);
+            hipLaunchKernelGGL((nc_md5_lines_kernel<true, kAuxNt>), dim3((unsigned)grid), dim3(256), 0, stream,
+                               d_keys, d_off, nkeys, d_out, ntiles, chunk);
         else if (il)
             hipLaunchKernelGGL(nc_md5_lines_kernel<true>, dim3((unsigned)grid), dim3(256), 0, stream, d_keys, d_off,
                                nkeys, d_out, ntiles, chunk);
