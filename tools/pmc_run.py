@@ -19,12 +19,16 @@ def main():
     ap.add_argument("--variant", default="0:0:0", help="grid_cap:sort:var")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--nkeys", type=int, default=0)
+    ap.add_argument("--lib", default="", help="another build of libnc_gpuhash.so (A/B builds)")
     args = ap.parse_args()
 
     import torch
 
-    import twemproxy_amd as t
     from twemproxy_amd import _lib as L
+
+    if args.lib:
+        L.LIB_PATH = os.path.abspath(args.lib)
+    import twemproxy_amd as t
 
     if args.config == "C4S":  # one GPU's C4 shard, as bench.py's c4_shard leg
         cfg = {"spec": t.CONFIGS["C4"]["spec"], "nkeys": 1 << 25}
