@@ -440,24 +440,21 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_short_kernel(const uint8_
         uint64_t s0;
     };
     auto key0 = [&](uint32_t j) { return tiles.at(j < n ? j : n - 1u) * 64u; };
-#ifndef NC_SHORT_OFF_AUX /* A/B builds only: the offsets' cache policy */
-#define NC_SHORT_OFF_AUX kAuxNt
-#endif
     auto load_off = [&](uint32_t j) __attribute__((always_inline)) {
         const uint32_t k0 = key0(j);
         const rsrc_t r = make_rsrc(off + k0, ((uint64_t)(nk32 - k0) + 1u) * 8u);
         Offs o;
         if constexpr (kVB) {
-            const u32x2 sv = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(lane * 8u), 0, NC_SHORT_OFF_AUX);
+            const u32x2 sv = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(lane * 8u), 0, kAuxNt);
             o.s = sv.x;
             o.s_hi = sv.y;
             o.s0 = 0;
         } else {
-            o.s = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u), 0, NC_SHORT_OFF_AUX);
+            o.s = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u), 0, kAuxNt);
             o.s_hi = 0;
             o.s0 = off[k0];
         }
-        o.e = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u + 8u), 0, NC_SHORT_OFF_AUX);
+        o.e = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(lane * 8u + 8u), 0, kAuxNt);
         return o;
     };
     auto base_of = [&](const Offs &o) __attribute__((always_inline)) {

@@ -793,10 +793,7 @@ __device__ __forceinline__ void gs_issue_offs(const uint64_t *__restrict__ off, 
     if (t < 3u) {
         const uint64_t e = k0 + gs_tile_count<TK>(tile, nkeys);
         const uint32_t *src = t == 0u ? o32 + 2u * e : t == 1u ? o32 + 2u * e + 1u : o32 + 2u * k0 + 1u;
-#ifndef NC_GS_BOUND_AUX /* A/B builds only: the three bound dwords' cache policy */
-#define NC_GS_BOUND_AUX AUX
-#endif
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)src, (lds_void_t *)(slot + 4u * TK), 4, 0, NC_GS_BOUND_AUX);
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)src, (lds_void_t *)(slot + 4u * TK), 4, 0, AUX);
     }
 }
 
