@@ -64,6 +64,18 @@ def note(*a):
         log(*a)
 
 
+T0 = time.monotonic()
+
+
+class Record(dict):
+    """the bench record; with --verbose each leg's arrival is a progress note
+    (a long multi-rank run otherwise prints nothing until its line)"""
+
+    def __setitem__(self, k, v):
+        super().__setitem__(k, v)
+        note(f"bench.py rank {os.environ.get('RANK', '0')}: {k} at {time.monotonic() - T0:.1f} s")
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -621,7 +633,8 @@ def main():
     rf = roofline(alg, kern_ms, load_traffic("fnv1a_64", "C2"))
     read_ceiling(t, rf, keys)
 
-    res = {
+    note(f"bench.py rank {rank}: C2 headline at {time.monotonic() - T0:.1f} s")
+    res = Record({
         "metric": METRIC, "value": round(value, 1), "unit": "Mkeys/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
@@ -634,7 +647,7 @@ def main():
         "kernel_ms_rank0": round(kern_ms, 4), "kernel_ms_max": round(kern_ms_max, 4),
         "variant": t.pick_variant("fnv1a_64", nk, shape),
         "roofline": rf,
-    }
+    })
     if scatter:
         res["scatter"] = scatter
     parity = {}
