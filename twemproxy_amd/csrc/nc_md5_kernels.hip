@@ -102,13 +102,7 @@ __device__ __forceinline__ void tail_entry(const uint32_t *qw, uint32_t slot, ui
     w[14] = len << 3;
     w[15] = len >> 29;
     /* words 1..13 are zero: folded into the steps' constants */
-#ifdef NC_MD5_TAIL_DIAG /* DIAGNOSTIC A/B builds only: the tail results kept in LDS, not stored (wrong outputs) */
-    asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)(qw + slot)), "v"(md5_tail_final_a(st, w)) : "memory");
-    (void)out;
-    (void)idx;
-#else
     __builtin_nontemporal_store(md5_tail_final_a(st, w), out + idx);
-#endif
 }
 
 __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__restrict__ out)
