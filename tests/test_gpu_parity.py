@@ -510,6 +510,41 @@ def test_wsort_ragged_tiles(gpu, oracle, var):
         L.lib().nc_gpuhash_set_tuning(0, 0, 0)
 
 
+@pytest.mark.parametrize("var", [0, (1 << 19) | (1 << 15) | (1 << 12), (1 << 19) | (1 << 15) | (1 << 12) | (1 << 14)],
+                         ids=["policy", "fullline_s64", "fullline_generic"])
+def test_md5_short_key_form(gpu, oracle, var):
+    """md5's S64 form (round 6: the caller's shape says no key exceeds 64
+    bytes, so every key is one data block and the rounds keep no chaining
+    state) on ragged batches of Zipf / uniform keys with empty keys, 55- to
+    64-byte keys (their tail blocks) and a misaligned buffer; and with shapes
+    that understate the longest key (a wave meeting a longer key leaves the
+    fast loop and runs the generic rounds from that tile: early in short
+    batches, late in a long one), against the oracle. Bit 14 turns the form
+    off (the generic rounds on the same shapes)."""
+    import torch
+
+    L.lib().nc_gpuhash_set_tuning(0, 0, var)
+    try:
+        cases = [(1, t.SynthSpec.zipf(70), None), (63, t.SynthSpec.zipf(71), None), (64, t.SynthSpec.zipf(72), None),
+                 (65, t.SynthSpec.uniform(73, 0, 64), None), (4097, t.SynthSpec.zipf(74), None),
+                 (70001, t.SynthSpec.uniform(75, 50, 64), None), (70001, t.SynthSpec.zipf(76), None),
+                 (9000, t.SynthSpec.uniform(77, 0, 100), 64),   # the shape says <= 64: wrong in most tiles
+                 (300000, t.SynthSpec.uniform(78, 0, 66), 64),  # wrong in a few tiles of a long batch
+                 (5000, t.SynthSpec.uniform(79, 60, 200), 64)]  # wrong from the first tile
+        for n, spec, claim in cases:
+            keys, off = t.synth_host(spec, 3, n)
+            lens = np.diff(off)
+            hi = int(lens.max()) if claim is None else claim
+            for shift in (0, 5):
+                kd, od = to_dev(keys, off, shift=shift)
+                got = t.hash_batch_device(1, kd, od, shape=(int(off[-1]), int(lens.min()), hi))
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), oracle.batch(1, keys, off),
+                                              err_msg=f"var={var} n={n} spec={spec} claim={claim} shift={shift}")
+    finally:
+        L.lib().nc_gpuhash_set_tuning(0, 0, 0)
+
+
 @pytest.mark.parametrize("fl", [16, 20, 24, 32, 40, 48])
 def test_md5_fixed_length_specialisation(gpu, oracle, fl):
     """md5's fixed-length instantiations (picked by a shape whose min == max)

@@ -1901,7 +1901,7 @@ namespace nc_md5 {
 /* md5 on the direct per-lane block pipeline (nc_md5_kernels.hip); keys is any
  * byte address, nkeys < 2^32 */
 hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
-                  int var, uint32_t fl);
+                  int var, uint32_t fl, uint32_t max_len);
 } // namespace nc_md5
 
 namespace nc_bytes {
@@ -1958,8 +1958,9 @@ constexpr int kVarDirect8 = 1 << 12;     /* line image: eight-wave workgroups, o
 constexpr int kVarDirectS8 = 1 << 13;    /* crcs: slicing-by-8 tables */
 constexpr int kVarDirectNoHash = 1 << 14; /* DIAGNOSTIC (fnv1a_64, crc32): xor of words, not a hash */
 constexpr int kVarMd5PadTab = 1 << 15;    /* md5: padding selectors from an LDS table */
-constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores; bit 13
-                                             (the crcs' S8) A/B: the line kernel's offsets non-temporal */
+constexpr int kVarMd5FullLines = 1 << 12; /* md5 (shares kVarDirect8's bit): whole-line output stores; A/B:
+                                             bit 13 (the crcs' S8) the line kernel's offsets non-temporal,
+                                             bit 14 (NoHash) no S64 form for shapes of keys <= 64 B */
 constexpr int kVarDirectShort = 1 << 11;  /* byte modes, keys <= 32 B: eight waves per CU, tiles in flight */
 constexpr int kVarDirectPairs = 1 << 10;  /* with kVarDirect8: the line image in rounds of two lines */
 constexpr int kVarDirectOffDefault = 1 << 9; /* A/B (crc32, fnv1a_64): the offsets with the default cache policy
@@ -2569,8 +2570,11 @@ hipError_t launch(int mode, const uint8_t *d_keys, const uint64_t *d_off, uint64
             return nc_md5::launch(d_keys, d_off, nkeys, d_out, stream,
                                   ((var >> 20) & 15) | ((var & kVarMd5PadTab) != 0 ? 16 : 0) |
                                       ((var & kVarMd5FullLines) != 0 ? 32 : 0) |
-                                      ((var & kVarDirectS8) != 0 ? 64 : 0),
-                                  fl);
+                                      ((var & kVarDirectS8) != 0 ? 64 : 0) | ((var & kVarDirectNoHash) != 0 ? 128 : 0),
+                                  fl,
+                                  shape != nullptr && nkeys != 0 && shape->max_len <= 0xffffffffull
+                                      ? (uint32_t)shape->max_len
+                                      : 0xffffffffu);
         }
         const bool short_words = (var & kVarDirectShort) != 0 && nc_bytes::supports_short_words(mode) &&
                                  shape != nullptr && nkeys != 0 && shape->max_len <= 32u;

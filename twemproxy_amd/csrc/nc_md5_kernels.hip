@@ -84,8 +84,8 @@ __device__ __forceinline__ uint32_t lanemask_lt_popc(uint64_t m)
  * key (empty, or longer than 64 bytes) carries its chaining state in X. */
 __device__ __forceinline__ void tail_entry(const uint32_t *qw, uint32_t slot, uint32_t *__restrict__ out)
 {
-    uint32_t st[4] = {qw[0 * kQ + slot], qw[1 * kQ + slot], qw[2 * kQ + slot], qw[3 * kQ + slot]};
     const uint32_t len = qw[4 * kQ + slot], idx = qw[5 * kQ + slot];
+    uint32_t st[4] = {qw[0 * kQ + slot], qw[1 * kQ + slot], qw[2 * kQ + slot], qw[3 * kQ + slot]};
     if (len - 56u <= 8u) {
         uint32_t w[16];
         w[11] = qw[6 * kQ + slot];
@@ -158,7 +158,14 @@ __device__ __forceinline__ void flush_tails(uint32_t *qmem, uint32_t (*qmeta)[2]
  * key i = keys[off[i], off[i+1]); keys stays readable NC_GPUHASH_PAD bytes
  * past off[nkeys]. A tile of 64 keys spans less than 4 GiB.
  */
-template <bool LDS, bool IL, int FL = 0, bool PT = false, bool FS = false>
+/* S64: the caller's shape says every key has at most 64 bytes (C2): one
+ * data block per key, so no round ever continues a key — no chaining state,
+ * no block-index bookkeeping, no second gen copy (and their loop-carried
+ * register copies). Each round checks its tile (one compare and a ballot);
+ * a tile with a longer key (a wrong shape) ends the fast loop, and that
+ * tile and the wave's later ones run the generic rounds: slower, never
+ * wrong. */
+template <bool LDS, bool IL, int FL = 0, bool PT = false, bool FS = false, bool S64 = false>
 __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__restrict__ keys,
                                                            const uint64_t *__restrict__ off, uint64_t nkeys,
                                                            uint32_t *__restrict__ out, uint64_t ntiles, uint32_t chunk)
@@ -217,8 +224,18 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
      * block — is read by the steps in place: with one set it had to be copied
      * out before the next round's loads could land there (24 v_mov per round
      * in the fixed-length form). */
-    auto round = [&](u32x4 (&cur)[4], u32x4 (&nxt)[4]) __attribute__((always_inline)) {
-        const bool more = ballot((lane < cur_t.nv) && cur_t.len > 64u * (b + 1u)) != 0ull;
+    bool bail = false; /* S64: this wave met a key longer than 64 bytes */
+    auto round = [&](auto fast_c, u32x4 (&cur)[4], u32x4 (&nxt)[4]) __attribute__((always_inline)) {
+        constexpr bool S = decltype(fast_c)::value;
+        bool more = false;
+        if constexpr (S) {
+            if (ballot((lane < cur_t.nv) && cur_t.len > 64u) != 0ull) {
+                bail = true; /* nothing of this tile consumed yet */
+                return;
+            }
+        } else {
+            more = ballot((lane < cur_t.nv) && cur_t.len > 64u * (b + 1u)) != 0ull;
+        }
         const TileKeys nxt_t = wk.keys_of(tile + 1u, no);
         const int32_t rem = (int32_t)cur_t.len - 64 * (int32_t)b; /* key bytes from this block's start */
         const uint32_t len = cur_t.len;
@@ -227,7 +244,8 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
          * keys) queue their state for a data-free tail block; the mask is
          * taken here, under the full exec mask (inside the steps' divergent
          * region hipcc rebuilds it with a select and a compare) */
-        const bool tail = (lane < cur_t.nv) && ((rem <= 64 && rem >= 56) || (b == 0u && len == 0u));
+        const bool tail = (lane < cur_t.nv) && (S ? (len >= 56u || len == 0u)
+                                                  : ((rem <= 64 && rem >= 56) || (b == 0u && len == 0u)));
         const uint64_t tm = ballot(tail);
         if constexpr (LDS) wk.read_img(img, cur); /* this round's block, DMA'd during the previous round */
         /* FL: a tile whose keys all have FL bytes (checked: the shape only
@@ -304,7 +322,7 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                     __builtin_amdgcn_raw_buffer_store_b32((FIRST ? NC_MD5_A0 : st[0]) + v[0], rout, (int)(lane * 4u),
                                                           0, kAuxNt);
                 }
-                if (fin) {
+                if (fin || S) { /* (S: a key of 56..64 bytes queues its tail block) */
                 } else if (len - 56u > 8u) {
                     md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
                     st[0] = (FIRST ? NC_MD5_A0 : st[0]) + v[0];
@@ -329,6 +347,8 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                     st[3] = NC_MD5_D0;
                 }
                 v = gen(std::false_type{});
+            } else if constexpr (S) {
+                v = gen(std::true_type{});
             } else {
                 v = b == 0u ? gen(std::true_type{}) : gen(std::false_type{});
             }
@@ -367,11 +387,27 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
             cur_t = nxt_t;
         }
     };
-    for (;;) {
-        round(da, db);
-        if (tile >= tlast) break;
-        round(db, da);
-        if (tile >= tlast) break;
+    if constexpr (S64) {
+        for (;;) {
+            round(std::true_type{}, da, db);
+            if (bail || tile >= tlast) break;
+            round(std::true_type{}, db, da);
+            if (bail || tile >= tlast) break;
+        }
+    }
+    if (!S64 || bail) {
+        if constexpr (S64) { /* the generic rounds from this tile: its offsets and block 0 again */
+            cur_t = wk.keys_of(tile, wk.template load_off<0>(tile));
+            no = wk.template load_off<0>(tile + 1u);
+            load_blk(cur_t, 0u, da);
+            b = 0u;
+        }
+        for (;;) {
+            round(std::false_type{}, da, db);
+            if (tile >= tlast) break;
+            round(std::false_type{}, db, da);
+            if (tile >= tlast) break;
+        }
     }
     }
     /* (pooled for the generic kernel; the fixed-length instantiations queue
@@ -494,13 +530,15 @@ void launch_fl(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uin
  * variant (long keys); bit 3 tiles interleaved over the grid; bit 4 the
  * padding selectors from the LDS table (pad_block_tab); bit 5 whole-line
  * stores (placeholders for the tail keys, FS); bit 6 (A/B) the line kernel's
- * offsets non-temporal (OA, the round-5 form). fl: the batch's
+ * offsets non-temporal (OA, the round-5 form); bit 7 (A/B) no S64 form.
+ * max_len: the caller's shape's longest key (0xffffffff: unknown); at most
+ * 64 takes the S64 form (FS only).  fl: the batch's
  * fixed key length if the caller's shape says so (0: unknown or varying);
  * 16, 20, 24, 32, 40 and 48 have specialised instantiations (each tile still
  * checks its lengths) */
 template <bool PT>
 hipError_t launch_pt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out,
-                     hipStream_t stream, int var, uint32_t fl)
+                     hipStream_t stream, int var, uint32_t fl, uint32_t max_len)
 {
     static const uint32_t kChunk[4] = {16, 8, 32, 64};
     const uint32_t chunk = kChunk[var & 3];
@@ -531,6 +569,9 @@ hipError_t launch_pt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkey
         case 40: launch_fl<40, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
         default: launch_fl<48, PT>(d_keys, d_off, nkeys, d_out, stream, grid, ntiles, chunk); break;
         }
+    } else if ((var & 32) && max_len <= 64u && (var & 128) == 0) {
+        hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, 0, PT, true, true>), dim3((unsigned)grid), dim3(256), 0,
+                           stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
     } else if (var & 32) {
         hipLaunchKernelGGL((nc_md5_direct_kernel<false, false, 0, PT, true>), dim3((unsigned)grid), dim3(256), 0,
                            stream, d_keys, d_off, nkeys, d_out, ntiles, chunk);
@@ -542,10 +583,10 @@ hipError_t launch_pt(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkey
 }
 
 hipError_t launch(const uint8_t *d_keys, const uint64_t *d_off, uint64_t nkeys, uint32_t *d_out, hipStream_t stream,
-                  int var, uint32_t fl)
+                  int var, uint32_t fl, uint32_t max_len)
 {
-    return (var & 16) ? launch_pt<true>(d_keys, d_off, nkeys, d_out, stream, var, fl)
-                      : launch_pt<false>(d_keys, d_off, nkeys, d_out, stream, var, fl);
+    return (var & 16) ? launch_pt<true>(d_keys, d_off, nkeys, d_out, stream, var, fl, max_len)
+                      : launch_pt<false>(d_keys, d_off, nkeys, d_out, stream, var, fl, max_len);
 }
 
 } // namespace nc_md5
