@@ -2442,7 +2442,10 @@ int pick_variant(int mode, uint64_t nkeys, const nc_gpuhash_shape *sh)
          * (profiles/r05_md5_padtab_ab.jsonl, pmc_r05_md5pt.json); and
          * whole-line output stores (the tail keys store a placeholder first,
          * nc_md5_kernels.hip FS): C2 0.7333 -> 0.7048 ms, same box, same
-         * process (profiles/r06f_md5_fullline_ab.jsonl) */
+         * process (profiles/r06f_md5_fullline_ab.jsonl); with a shape whose
+         * keys are <= 64 B, the S64 form (no chaining state): C2
+         * SQ_INSTS_VALU 400.7 M -> 383.4 M, 0.7184 -> 0.7123 ms
+         * (profiles/r06s_md5_s64_ab.jsonl, pmc_r06s_md5_s64_valu.json) */
         return kVarMd5Direct | (lds ? (12 << 20) : kVarMd5PadTab | kVarMd5FullLines);
     }
     if (sh == nullptr || nkeys == 0 || sh->key_bytes == 0) return kVarRegStaged;
