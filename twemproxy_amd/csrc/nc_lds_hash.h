@@ -33,16 +33,7 @@ struct LdsSrc {
     static constexpr bool kOverread = true; /* reads past a key stay inside LDS */
     const uint32_t *base; /* 16-byte aligned LDS slab, read as dwords */
     /* dwords i, i+1 (4-byte aligned): one ds_read2_b32 */
-#ifdef NC_LDS_B64 /* A/B builds only: one ds_read_b64 at a 4-byte-aligned address (the unaligned LDS mode) */
-    __device__ __forceinline__ uint2 d2(uint32_t i) const
-    {
-        typedef uint32_t u2a __attribute__((ext_vector_type(2), aligned(8)));
-        const u2a v = *reinterpret_cast<const u2a *>(base + i);
-        return make_uint2(v.x, v.y);
-    }
-#else
     __device__ __forceinline__ uint2 d2(uint32_t i) const { return make_uint2(base[i], base[i + 1]); }
-#endif
     __device__ __forceinline__ uint32_t d1(uint32_t i) const { return base[i]; }
 };
 
