@@ -878,8 +878,9 @@ def summarize(res: dict, detail_path: str | None) -> dict:
             line["c5_e2e"] = c5
         else:
             def pt(r_):
-                return None if r_ is None else {k: r_[k] for k in ("depth", "lanes", "threads", "submit_to_done_us",
-                                                                   "us_per_batch", "mkeys_s") if k in r_}
+                return None if r_ is None else {k: r_[k] for k in ("depth", "lanes", "threads", "staging",
+                                                                   "submit_to_done_us", "us_per_batch", "mkeys_s")
+                                                if k in r_}
             # one batch in flight: the faster worker shape (256- or 1024-thread lanes)
             ring1 = max((r_ for r_ in c5["gpu"] if r_["path"].startswith("ring") and r_["depth"] == 1),
                         key=lambda r_: r_["mkeys_s"], default=None)

@@ -303,7 +303,10 @@ rstatus_t nc_gpuhash_host_unregister(void *ptr);
 /* ---- 3d. small batches with no HIP call per batch: the batch ring ----
  * One mbuf's keys at a time (the batch site of src/nc_message.c:700-714 and
  * the fragment loops) without a kernel launch or an event per batch: the
- * ring's slots live in mapped, coherent host memory and ONE resident launch
+ * ring's slots live in mapped, coherent host memory — a ring of 1 or 2 lanes
+ * on a large-BAR device stages its batches in device memory the host writes
+ * through the BAR instead (NC_GPUHASH_RING_STAGING=host|device at create
+ * overrides) — and ONE resident launch
  * polls them (csrc/nc_ring.hip), one workgroup per lane: batch n belongs to
  * lane n % nlanes, each lane takes its batches in order, and the lanes'
  * PCIe round trips overlap. A submit copies the spans' bytes into the slot

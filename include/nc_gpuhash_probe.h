@@ -112,11 +112,15 @@ rstatus_t nc_gpuhash_ring_debug_hold(nc_gpuhash_ring_t *r, int hold);
 /* timeline: on = 1 before the first submit makes every batch record its
  * device timeline in its slot (s_memrealtime, 100 MHz): [0] descriptor
  * found, [1] batch staged in LDS, [2] every hash store issued, [3] stores
- * acknowledged, written before the done word; [4] done word stored and [5]
- * the lane's batch count, which reach host memory with the NEXT batch's
- * release. on = -1 only reads slot `slot`'s eight words into out (when out is
- * not NULL). */
+ * acknowledged, written before the done word; [4] hashes released (or, with
+ * write-through hashes, drained) and [5] the lane's batch count, stored just
+ * before the done word and possibly landing just after it. on = -1 only reads
+ * slot `slot`'s eight words into out (when out is not NULL). */
 rstatus_t nc_gpuhash_ring_debug_timeline(nc_gpuhash_ring_t *r, int on, uint32_t slot, uint64_t out[8]);
+/* where the ring stages its batches: 1 = device memory written through the
+ * PCIe BAR (large-BAR devices), 0 = mapped host memory (no large BAR, or
+ * NC_GPUHASH_RING_STAGING=host when the ring was created), -1 = NULL ring */
+int nc_gpuhash_ring_debug_staging(const nc_gpuhash_ring_t *r);
 
 #ifdef __cplusplus
 }

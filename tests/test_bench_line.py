@@ -41,7 +41,7 @@ def _full_record():
     res["c4_shard"] = {m: {"kernel_ms": 1.79, "value": 18681.2, "unit": "Mkeys/s", "roofline": _rf(0.627)}
                        for m in ("md5", "crc32", "fnv1a_64")}
     res["c4_shard"]["md5"]["roofline_valu"] = md5_rf
-    row = {"point": "gpu", "path": "ring (resident worker, mapped host memory)", "depth": 8, "lanes": 8,
+    row = {"point": "gpu", "path": "ring (resident worker)", "staging": "device", "depth": 8, "lanes": 8,
            "threads": 1024, "batches": 320245, "keys_per_batch": 585.1, "submit_to_done_us": 9.71,
            "mkeys_s": 468.46, "mismatches": 0, "worker_launches": 1}
     res["c5_e2e"] = {"host_per_key": {"point": "host", "path": "host", "mkeys_s": 80.81},

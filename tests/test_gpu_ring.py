@@ -1,9 +1,13 @@
 """The batch ring (nc_gpuhash_ring, include/nc_gpuhash.h 3d): small batches
-served by one resident launch (a workgroup per lane) polling mapped host
-memory, no HIP call per batch. Every result against the oracle; the launch's
-life cycle (one launch for a burst, ending after an idle 10 ms or 2 s and
-relaunching on demand, stopping on destroy), the lane and thread shapes, the
-ticket space across 2^31 and 2^32 batches, and the limits."""
+served by one resident launch (a workgroup per lane) polling its staging, no
+HIP call per batch. Every result against the oracle; the launch's life cycle
+(one launch for a burst, ending after an idle 10 ms or 2 s and relaunching on
+demand, stopping on destroy), the lane and thread shapes, the ticket space
+across 2^31 and 2^32 batches, and the limits. Every test runs twice: with the
+batches staged in device memory written through the PCIe BAR
+(NC_GPUHASH_RING_STAGING=device; the default for rings of 1 or 2 lanes on a
+large-BAR device such as the MI355X) and in mapped host memory
+(NC_GPUHASH_RING_STAGING=host; the default for 4 lanes and more)."""
 import ctypes
 import threading
 import time
@@ -14,6 +18,26 @@ import pytest
 import twemproxy_amd as t
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(120)]
+
+
+@pytest.fixture(autouse=True, params=["device", "host"])
+def staging(request, monkeypatch):
+    """the staging every ring of the test is created with (read at create)"""
+    monkeypatch.setenv("NC_GPUHASH_RING_STAGING", request.param)
+    return request.param
+
+
+def test_ring_staging_is_the_one_asked_for(gpu, staging):
+    # MI355X exposes its whole HBM through a large BAR (tools/probes/bar_probe.hip)
+    with t.Ring(0, nslots=2) as r:
+        assert r.staging == staging
+
+
+@pytest.mark.parametrize("lanes,want", [(1, "device"), (2, "device"), (4, "host"), (8, "host")])
+def test_ring_default_staging(gpu, staging, monkeypatch, lanes, want):
+    monkeypatch.delenv("NC_GPUHASH_RING_STAGING")
+    with t.Ring(0, nslots=8, lanes=lanes) as r:
+        assert r.staging == want
 
 
 def batch(rng, nkeys, maxlen=300, total=30000):
@@ -176,6 +200,22 @@ def test_ring_shared_by_threads(gpu, oracle):
     assert not errors, errors[0]
 
 
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_ring_tiny_batches(gpu, oracle, lanes):
+    """batches of 0..9 keys, every mode, one and two lanes"""
+    rng = np.random.default_rng(77 + lanes)
+    work = []
+    for nk in list(range(10)) * 2:
+        buf, spans = batch(rng, nk, maxlen=90)
+        m = int(rng.integers(0, 12))
+        work.append((m, buf, spans, want(oracle, m, buf, spans)))
+    with t.Ring(0, nslots=4, lanes=lanes, threads=1024) as r:
+        for m, buf, spans, w in work:
+            tk, out = r.submit_spans(m, buf, spans)
+            r.wait(tk)
+            np.testing.assert_array_equal(out, w, err_msg=f"{t.HASH_NAMES[m]} {len(spans)}")
+
+
 def test_ring_rejects_spans_outside_the_buffer(gpu):
     with t.Ring(0, nslots=2) as r:
         buf = np.zeros(100, np.uint8)
@@ -184,7 +224,8 @@ def test_ring_rejects_spans_outside_the_buffer(gpu):
                 r.submit_spans("fnv1a_64", buf, bad)
 
 
-@pytest.mark.parametrize("lanes,threads", [(1, 256), (2, 512), (3, 1024), (4, 256), (8, 256), (8, 1024)])
+@pytest.mark.parametrize("lanes,threads", [(1, 256), (1, 512), (1, 1024), (2, 256), (2, 512), (2, 1024), (3, 1024),
+                                           (4, 256), (8, 256), (8, 1024)])
 def test_ring_lane_shapes(gpu, oracle, lanes, threads):
     """every lane count and workgroup size, batches pipelined over 8 slots"""
     rng = np.random.default_rng(50 + lanes * 7 + threads)

@@ -73,8 +73,9 @@ static int cmp_d(const void *a, const void *b)
 /* one batch in flight through the batch ring, with the worker's timeline:
  * host submit call; device found -> staged (the batch fetched across PCIe
  * into LDS) -> issued (hashes computed, stores issued) -> stored (stores
- * acknowledged) -> released (done word stored; this stamp lands with the next
- * batch, so it is read one batch late); and the host's submit -> done.
+ * acknowledged) -> released (the release, or the write-through drain, before
+ * the done word; its stamp may land just after the done word, and then the
+ * batch counts 0 here); and the host's submit -> done.
  * Medians in microseconds. */
 static int ring_timeline(double seconds, struct mbuf *mb, uint32_t nmb, uint32_t maxk, const uint32_t *ref,
                          const uint32_t *first)
@@ -86,7 +87,7 @@ static int ring_timeline(double seconds, struct mbuf *mb, uint32_t nmb, uint32_t
     double *v[NV];
     for (int i = 0; i < NV; i++) v[i] = malloc(NMAX * sizeof(double));
     if (!outs) return 1;
-    uint64_t bad = 0, prev_stored = 0;
+    uint64_t bad = 0;
     int n = 0;
     const double tend = now_s() + seconds;
     for (uint32_t i = 0; n < NMAX && now_s() < tend; i++) {
@@ -101,7 +102,7 @@ static int ring_timeline(double seconds, struct mbuf *mb, uint32_t nmb, uint32_t
         for (uint32_t k = 0; k < mb[bi].nkeys; k++) bad += outs[k] != ref[first[bi] + k];
         uint64_t tl[8];
         if (nc_gpuhash_ring_debug_timeline(ring, -1, 0, tl) != NC_OK) return 1;
-        const uint64_t stored = tl[3], released_prev = tl[4];
+        const uint64_t stored = tl[3], released = tl[5] == (uint64_t)i + 1u ? tl[4] : 0; /* may land late: then 0 */
         if (i >= nmb) { /* past the warm-up (the first launch) */
             v[0][n] = (b - a) * 1e6;
             v[1][n] = (c - a) * 1e6;
@@ -109,23 +110,21 @@ static int ring_timeline(double seconds, struct mbuf *mb, uint32_t nmb, uint32_t
             v[3][n] = (double)(tl[2] - tl[1]) * 0.01;
             v[4][n] = (double)(tl[3] - tl[2]) * 0.01;
             v[5][n] = (double)(tl[3] - tl[0]) * 0.01;
-            /* the previous batch's release, which landed with this one */
-            v[6][n] = released_prev > prev_stored && prev_stored ? (double)(released_prev - prev_stored) * 0.01 : 0.0;
+            v[6][n] = released > stored ? (double)(released - stored) * 0.01 : 0.0;
             v[7][n] = v[1][n] - v[0][n] - v[5][n] - v[6][n];
             n++;
         }
-        prev_stored = stored;
     }
     double med[NV];
     for (int i = 0; i < NV; i++) {
         qsort(v[i], (size_t)n, sizeof(double), cmp_d);
         med[i] = n ? v[i][n / 2] : 0.0;
     }
-    printf("{\"point\": \"ring_timeline\", \"depth\": 1, \"threads\": %d, \"batches\": %d, \"median_us\": "
+    printf("{\"point\": \"ring_timeline\", \"staging\": \"%s\", \"depth\": 1, \"threads\": %d, \"batches\": %d, \"median_us\": "
            "{\"host_submit_call\": %.2f, \"submit_to_done\": %.2f, \"dev_fetch\": %.2f, \"dev_hash\": %.2f, "
            "\"dev_store_ack\": %.2f, \"dev_found_to_stored\": %.2f, \"dev_release\": %.2f, "
            "\"rest_detect_done_reap\": %.2f}, \"mismatches\": %" PRIu64 "}\n",
-           NC_GPUHASH_RING_DEFAULT_THREADS, n, med[0], med[1], med[2], med[3], med[4], med[5], med[6], med[7], bad);
+           nc_gpuhash_ring_debug_staging(ring) == 1 ? "device" : "host", NC_GPUHASH_RING_DEFAULT_THREADS, n, med[0], med[1], med[2], med[3], med[4], med[5], med[6], med[7], bad);
     nc_gpuhash_ring_destroy(ring);
     return bad ? 2 : 0;
 }
@@ -325,11 +324,12 @@ int main(int argc, char **argv)
             inflight++;
         }
         const double el = now_s() - t0;
-        printf("{\"point\": \"gpu\", \"path\": \"ring (resident worker, mapped host memory)\", \"depth\": %d, "
+        printf("{\"point\": \"gpu\", \"path\": \"ring (resident worker)\", \"staging\": \"%s\", \"depth\": %d, "
                "\"lanes\": %u, \"threads\": %u, "
                "\"batches\": %" PRIu64 ", \"keys_per_batch\": %.1f, \"submit_to_done_us\": %.2f, \"mkeys_s\": %.2f, "
                "\"mismatches\": %" PRIu64 ", \"worker_launches\": %" PRIu64 "}\n",
-               nslots, nc_gpuhash_ring_lanes(ring), rthreads[ti], batches, (double)done_keys / (double)batches,
+               nc_gpuhash_ring_debug_staging(ring) == 1 ? "device" : "host", nslots, nc_gpuhash_ring_lanes(ring),
+               rthreads[ti], batches, (double)done_keys / (double)batches,
                lat_sum / (double)batches * 1e6, (double)done_keys / el / 1e6, bad, nc_gpuhash_ring_launches(ring));
         fflush(stdout);
         if (bad) rc = 2;

@@ -95,6 +95,15 @@ int main()
                  {"hipExtMallocWithFlags Finegrained", 1, hipDeviceMallocFinegrained},
                  {"hipExtMallocWithFlags Uncached", 1, hipDeviceMallocUncached},
                  {"hipHostMalloc Mapped|Coherent (the ring's)", 2, 0}};
+    {
+        int v1 = -1, v2 = -1, v3 = -1, v4 = -1;
+        (void)hipDeviceGetAttribute(&v1, hipDeviceAttributeDirectManagedMemAccessFromHost, 0);
+        (void)hipDeviceGetAttribute(&v2, hipDeviceAttributePageableMemoryAccess, 0);
+        (void)hipDeviceGetAttribute(&v3, hipDeviceAttributeHostNativeAtomicSupported, 0);
+        (void)hipDeviceGetAttribute(&v4, hipDeviceAttributeCanUseHostPointerForRegisteredMem, 0);
+        printf("{\"probe\": \"bar_dev_attr\", \"direct_managed_from_host\": %d, \"pageable\": %d, "
+               "\"host_native_atomic\": %d, \"host_ptr_registered\": %d}\n", v1, v2, v3, v4);
+    }
     for (const Kind &k : kinds) {
         void *p = NULL, *pd = NULL;
         hipError_t e = hipSuccess;
@@ -110,6 +119,13 @@ int main()
         if (k.how == 2 && hipHostGetDevicePointer(&pd, p, 0) != hipSuccess) return 1;
         if (hipMemset(pd, 0, 1 << 20) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return 1;
         const int acc = host_access((volatile uint32_t *)p);
+        hipPointerAttribute_t pa;
+        memset(&pa, 0, sizeof(pa));
+        const hipError_t pe = hipPointerGetAttributes(&pa, p);
+        printf("{\"probe\": \"bar_attr\", \"memory\": \"%s\", \"rc\": %d, \"type\": %d, \"device_ptr\": %d, "
+               "\"host_ptr\": %d, \"host_eq_dev\": %d, \"is_managed\": %d, \"alloc_flags\": %u}\n",
+               k.name, (int)pe, (int)pa.type, pa.devicePointer != NULL, pa.hostPointer != NULL,
+               pa.hostPointer == pa.devicePointer, pa.isManaged, pa.allocationFlags);
         double stage_us = -1.0, rt_us = -1.0;
         uint32_t got = 0, npoll = 0;
         if (acc) {

@@ -152,6 +152,7 @@ SIGNATURES = {
         [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32],
     ),
     "nc_gpuhash_ring_lanes": (ctypes.c_uint32, [ctypes.c_void_p]),
+    "nc_gpuhash_ring_debug_staging": (ctypes.c_int, [ctypes.c_void_p]),
     "nc_gpuhash_ring_debug_start_seq": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "nc_gpuhash_ring_debug_hold": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "nc_gpuhash_ring_debug_timeline": (

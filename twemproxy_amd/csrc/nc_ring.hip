@@ -39,6 +39,23 @@
  *     thread 0 issues one system-scope release and the slot's done word.
  *   host poll: one load of that word; the hashes are copied to the caller.
  *
+ * Staging in device memory: where the host can store into the device's HBM
+ * through the PCIe BAR (a large-BAR device, hipDeviceAttributeIsLargeBar),
+ * the host-written, device-read words — descriptors, key spans, key images
+ * and the `stop` word — live in ONE uncached device allocation instead: the
+ * host's memcpy crosses PCIe as posted writes (write-combined, ~0.8 us for a
+ * C5 mbuf's 15.4 KB, tools/probes/bar_probe.hip), and the worker's poll and
+ * fetch read HBM instead of crossing PCIe and back (the round trip of a flag
+ * 1.75-2.1 us against 2.5-2.6 us in host memory, the same probe). Uncached:
+ * the host rewrites a slot between batches behind L2's back, so no read of
+ * that memory may hit a line L2 kept. The device-written words (done,
+ * outputs, `exiting`, `processed`) stay in mapped host memory, where the
+ * host's poll is a local load. NC_GPUHASH_RING_STAGING=host keeps everything
+ * in host memory (the A/B, and devices without a large BAR). By default only
+ * rings of 1 or 2 lanes stage in device memory: the host's stores through the
+ * BAR cost it ~0.5 us more per C5 batch than a memcpy into host memory,
+ * which is what bounds a ring of 4 and more lanes.
+ *
  * The launch always ends: on `stop`; and once any lane finds the whole ring
  * idle for kIdleTicks, or the launch older than kLifeTicks (checked when
  * idle and after every batch, and honoured before the next batch is taken,
@@ -82,7 +99,7 @@ static_assert(kMaxLanes == NC_GPUHASH_RING_MAX_LANES, "header limit");
 /* a lane's control block in mapped host memory: host-written and
  * device-written words on their own 128-byte lines */
 struct RingCtl {
-    uint32_t stop; /* host: 1 = the worker returns at its next poll */
+    uint32_t stop; /* host: 1 = the worker returns at its next poll (host staging) */
     uint32_t pad0[31];
     uint32_t exiting;   /* device: 1 from the moment the lane's worker decides to leave */
     uint32_t pad1;
@@ -141,16 +158,33 @@ __device__ __forceinline__ void release_sys()
 
 __device__ __forceinline__ uint64_t ticks() { return wall_clock64(); } /* s_memrealtime, 100 MHz */
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+/* 16 hash bytes into the slot's mapped output, write-through (sc0 sc1: the
+ * system-scope store form), so that the storing wave's vmcnt(0) wait alone
+ * orders them before the done word — no L2 write-back (MI355X_MICROARCH.md,
+ * hand-off forms: sc0 sc1 stores, every storing wave drained, a barrier, one
+ * lane's flag). One fabric write per 16 bytes, not per 4 (a C5 batch: 147
+ * PCIe writes instead of 585). */
+__device__ __forceinline__ void st_out4(__amdgpu_buffer_rsrc_t rsrc, uint32_t q, u32x4 v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, q * 16u, 0, 17 /* sc0 sc1 */);
+}
+
 /* the batch's keys, thread t taking keys t, t + T, ...: each read from the
  * LDS image by the realigning reader (which may read up to 22 bytes past a
- * key: the image's NC_GPUHASH_PAD tail) */
+ * key: the image's NC_GPUHASH_PAD tail). Each hash goes to the mapped output
+ * (plain stores, published by the release before the done word), or with
+ * `wt` in place of its span word in LDS, for one write-through pass out. */
 template <int MODE, uint32_t T>
-__device__ __forceinline__ void serve(const LdsSrc &src, const uint32_t *loff, uint32_t nk, const uint32_t *tab,
-                                      uint32_t *so_out)
+__device__ __forceinline__ void serve(const LdsSrc &src, uint32_t *loff, uint32_t nk, const uint32_t *tab,
+                                      uint32_t *so_out, bool wt)
 {
     for (uint32_t i = threadIdx.x; i < nk; i += T) {
         const uint32_t sp = loff[i]; /* start | end << 16 in the image */
-        so_out[i] = hash_key<MODE, 0>(src, sp & 0xffffu, (sp >> 16) - (sp & 0xffffu), tab);
+        const uint32_t h = hash_key<MODE, 0>(src, sp & 0xffffu, (sp >> 16) - (sp & 0xffffu), tab);
+        if (wt) loff[i] = h;
+        else so_out[i] = h;
     }
 }
 
@@ -158,9 +192,9 @@ __device__ __forceinline__ void serve(const LdsSrc &src, const uint32_t *loff, u
 struct Poll {
     uint64_t d;
     uint32_t stop, closing;
-    __device__ __forceinline__ void issue(RingCtl *c, const uint64_t *dp, RingDev *dv)
+    __device__ __forceinline__ void issue(const uint32_t *stopw, const uint64_t *dp, RingDev *dv)
     {
-        stop = ld_rlx(&c->stop);
+        stop = ld_rlx(stopw);
         d = ld_rlx64(dp);
         closing = __hip_atomic_load(&dv->closing, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -215,18 +249,22 @@ __device__ __forceinline__ int poll_check(const Poll &p, uint32_t tag, uint32_t 
 /* one launch, one workgroup per lane (lane = blockIdx.x): lane g's batches
  * are seq = k * nlanes + g for k = processed, processed + 1, ... */
 template <uint32_t T>
-__global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, const uint64_t *desc, uint32_t *done,
+__global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, const uint32_t *stopw,
+                                                    uint32_t stop_stride, const uint64_t *desc, uint32_t *done,
                                                     const uint32_t *offs, const uint8_t *keys, uint32_t *outs,
                                                     uint32_t nslots, uint32_t max_keys, uint64_t kstride,
-                                                    uint32_t nlanes, uint32_t epoch, uint64_t *tl)
+                                                    uint32_t nlanes, uint32_t epoch, uint32_t flags, uint64_t *tl)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
     __shared__ uint32_t crc16t[256], crc32t[256];
     __shared__ uint32_t cmd[2]; /* go, the descriptor's low word */
     const uint32_t t = threadIdx.x, lane = blockIdx.x;
     RingCtl *c = ctl + lane;
+    const uint32_t *stop_lane = stopw + (uint64_t)lane * stop_stride; /* the lane's `stop`, or the ring's one word */
     uint32_t *loff = reinterpret_cast<uint32_t *>(dyn);
     uint8_t *lkeys = dyn + ((4u * (max_keys + 1u) + 15u) & ~15u);
+    const bool wt = (flags & 1u) != 0u;
+    const uint32_t ostride = (max_keys + 3u) & ~3u; /* outputs: 16-byte aligned slots */
     for (uint32_t i = t; i < 256u; i += T) {
         crc16t[i] = nc_crc16_entry(i);
         crc32t[i] = nc_crc32_entry(i);
@@ -251,7 +289,7 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
              * (measured: depth 1 7.3-7.9 -> 8.1-8.7 us) */
             for (;;) {
                 Poll p;
-                p.issue(c, desc + s, dv);
+                p.issue(stop_lane, desc + s, dv);
                 const int r = poll_check(p, tag, epoch, expired, last, leaving, last_taken, c, dv, go, lo);
                 if (r > 0) break;
                 if (r == 0) __builtin_amdgcn_s_sleep(2);
@@ -266,11 +304,10 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
         __syncthreads();
         if (cmd[0] == 0u) break;
         const uint32_t mode = cmd[1] & 15u, nk = (cmd[1] >> 4) & 0xfffu, nb = cmd[1] >> 16;
-        /* the slot's key spans and image into LDS: coalesced reads across
-         * PCIe that bypass the caches (the host rewrote them), every load of
-         * a thread issued before its first LDS write, so the workgroup pays
-         * one PCIe round trip */
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        /* the slot's key spans and image into LDS: coalesced reads (across
+         * PCIe, or from uncached HBM with device staging) that bypass the
+         * caches (the host rewrote them), every load of a thread issued
+         * before its first LDS write, so the workgroup pays one round trip */
         const uint32_t *so = offs + (uint64_t)s * max_keys;
         const u32x4 *sk = reinterpret_cast<const u32x4 *>(keys + (uint64_t)s * kstride);
         const uint32_t nq = (nb + 15u) / 16u;
@@ -290,21 +327,26 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
             if (t + j * T < nq) reinterpret_cast<u32x4 *>(lkeys)[t + j * T] = kv[j];
         __syncthreads();
         if (tl != nullptr && t == 0u) t_staged = ticks();
-        uint32_t *so_out = outs + (uint64_t)s * max_keys;
+        uint32_t *so_out = outs + (uint64_t)s * ostride;
         const LdsSrc src{reinterpret_cast<const uint32_t *>(lkeys)};
         switch (mode) {
-        case NC_GPUHASH_ONE_AT_A_TIME: serve<NC_GPUHASH_ONE_AT_A_TIME, T>(src, loff, nk, crc32t, so_out); break;
-        case NC_GPUHASH_MD5: serve<NC_GPUHASH_MD5, T>(src, loff, nk, crc32t, so_out); break;
-        case NC_GPUHASH_CRC16: serve<NC_GPUHASH_CRC16, T>(src, loff, nk, crc16t, so_out); break;
-        case NC_GPUHASH_CRC32: serve<NC_GPUHASH_CRC32, T>(src, loff, nk, crc32t, so_out); break;
-        case NC_GPUHASH_CRC32A: serve<NC_GPUHASH_CRC32A, T>(src, loff, nk, crc32t, so_out); break;
-        case NC_GPUHASH_FNV1_64: serve<NC_GPUHASH_FNV1_64, T>(src, loff, nk, crc32t, so_out); break;
-        case NC_GPUHASH_FNV1A_64: serve<NC_GPUHASH_FNV1A_64, T>(src, loff, nk, crc32t, so_out); break;
-        case NC_GPUHASH_FNV1_32: serve<NC_GPUHASH_FNV1_32, T>(src, loff, nk, crc32t, so_out); break;
-        case NC_GPUHASH_FNV1A_32: serve<NC_GPUHASH_FNV1A_32, T>(src, loff, nk, crc32t, so_out); break;
-        case NC_GPUHASH_HSIEH: serve<NC_GPUHASH_HSIEH, T>(src, loff, nk, crc32t, so_out); break;
-        case NC_GPUHASH_MURMUR: serve<NC_GPUHASH_MURMUR, T>(src, loff, nk, crc32t, so_out); break;
-        default: serve<NC_GPUHASH_JENKINS, T>(src, loff, nk, crc32t, so_out); break;
+        case NC_GPUHASH_ONE_AT_A_TIME: serve<NC_GPUHASH_ONE_AT_A_TIME, T>(src, loff, nk, crc32t, so_out, wt); break;
+        case NC_GPUHASH_MD5: serve<NC_GPUHASH_MD5, T>(src, loff, nk, crc32t, so_out, wt); break;
+        case NC_GPUHASH_CRC16: serve<NC_GPUHASH_CRC16, T>(src, loff, nk, crc16t, so_out, wt); break;
+        case NC_GPUHASH_CRC32: serve<NC_GPUHASH_CRC32, T>(src, loff, nk, crc32t, so_out, wt); break;
+        case NC_GPUHASH_CRC32A: serve<NC_GPUHASH_CRC32A, T>(src, loff, nk, crc32t, so_out, wt); break;
+        case NC_GPUHASH_FNV1_64: serve<NC_GPUHASH_FNV1_64, T>(src, loff, nk, crc32t, so_out, wt); break;
+        case NC_GPUHASH_FNV1A_64: serve<NC_GPUHASH_FNV1A_64, T>(src, loff, nk, crc32t, so_out, wt); break;
+        case NC_GPUHASH_FNV1_32: serve<NC_GPUHASH_FNV1_32, T>(src, loff, nk, crc32t, so_out, wt); break;
+        case NC_GPUHASH_FNV1A_32: serve<NC_GPUHASH_FNV1A_32, T>(src, loff, nk, crc32t, so_out, wt); break;
+        case NC_GPUHASH_HSIEH: serve<NC_GPUHASH_HSIEH, T>(src, loff, nk, crc32t, so_out, wt); break;
+        case NC_GPUHASH_MURMUR: serve<NC_GPUHASH_MURMUR, T>(src, loff, nk, crc32t, so_out, wt); break;
+        default: serve<NC_GPUHASH_JENKINS, T>(src, loff, nk, crc32t, so_out, wt); break;
+        }
+        if (wt) { /* the hashes, in LDS, out 16 bytes a lane (up to 3 words past nk: within the slot's ostride) */
+            __syncthreads();
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(so_out, 0, 4u * ostride, 0x00020000);
+            for (uint32_t q = t; q < (nk + 3u) / 4u; q += T) st_out4(rs, q, reinterpret_cast<const u32x4 *>(loff)[q]);
         }
         if (tl != nullptr) { /* diagnostics: every thread's hashes issued (stores not yet acknowledged) */
             __syncthreads();
@@ -314,13 +356,18 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
         __syncthreads();                /* ... in every wave ... */
         done_count++;
         if (t == 0u) { /* ... then one system-scope release for the workgroup before the slot reads as done */
-            if (tl != nullptr) { /* found, staged, issued, stored: covered by the release below */
-                tl[8 * s + 0] = t_found;
-                tl[8 * s + 1] = t_staged;
-                tl[8 * s + 2] = t_issued;
-                tl[8 * s + 3] = ticks();
+            if (tl != nullptr) { /* found, staged, issued, stored: ordered by the release (or drain) below */
+                __hip_atomic_store(&tl[8 * s + 0], (uint64_t)(t_found), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&tl[8 * s + 1], (uint64_t)(t_staged), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&tl[8 * s + 2], (uint64_t)(t_issued), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&tl[8 * s + 3], (uint64_t)(ticks()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
-            release_sys();
+            if (wt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* the hashes went through: acknowledged above */
+            else release_sys();
+            if (tl != nullptr) { /* released (or drained); these two may land just after the done word */
+                __hip_atomic_store(&tl[8 * s + 4], ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&tl[8 * s + 5], done_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             /* relaxed stores after the fence: a release store would wait for
              * the write-back again. `processed` is read by the host only
              * once the launch has ended */
@@ -329,10 +376,6 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
             last = ticks();
             expired = last - born > kLifeTicks;
             __hip_atomic_fetch_max(&dv->last, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (tl != nullptr) { /* released; visible with the next batch's release */
-                tl[8 * s + 4] = last;
-                tl[8 * s + 5] = done_count;
-            }
         }
         tag = kTagBit | ((tag + nlanes) & kTagMask);
         s += nlanes;
@@ -340,8 +383,9 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
     }
 }
 
-typedef void (*worker_fn)(RingCtl *, RingDev *, const uint64_t *, uint32_t *, const uint32_t *, const uint8_t *,
-                          uint32_t *, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t, uint64_t *);
+typedef void (*worker_fn)(RingCtl *, RingDev *, const uint32_t *, uint32_t, const uint64_t *, uint32_t *,
+                          const uint32_t *, const uint8_t *, uint32_t *, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t,
+                          uint32_t, uint64_t *);
 
 enum { SLOT_FREE = 0, SLOT_RUNNING = 1 };
 
@@ -351,7 +395,11 @@ struct nc_gpuhash_ring {
     int device;
     uint32_t nslots, max_keys, nlanes, threads;
     uint64_t max_key_bytes, kstride;
-    uint8_t *host; /* one mapped, coherent allocation: ctl[kMaxLanes], desc, done, offsets, keys, outputs */
+    uint8_t *host; /* one mapped, coherent allocation: ctl[kMaxLanes], done, outputs (+ desc, offsets, keys) */
+    uint8_t *stage; /* device staging (large BAR): the stop word, desc, offsets, keys; NULL = all in host */
+    uint32_t *stopw, *d_stopw; /* the words the workers poll for `stop` */
+    uint32_t stop_stride;      /* in words, between lanes' stop words (0: one word for all) */
+    uint32_t flags;            /* the worker's: bit 0 = write-through hashes (st_out4), no release before done */
     RingCtl *ctl, *d_ctl; /* one per lane */
     uint64_t *desc, *d_desc;
     uint32_t *done, *d_done, *offs, *d_offs, *outs, *d_outs;
@@ -379,9 +427,9 @@ static rstatus_t ring_fail(hipError_t e)
     return errno == ENOMEM ? NC_ENOMEM : NC_ERROR;
 }
 
-/* the LDS of a lane: span words, the key image, and 96 bytes for the
- * realigning reader's look-ahead (md5's final block reads up to 86 bytes past
- * its start, nc_lds_hash.h) */
+/* the LDS of a lane: span words (then the hashes), the key image, and 96
+ * bytes for the realigning reader's look-ahead (md5's final block reads up to
+ * 86 bytes past its start, nc_lds_hash.h) */
 static size_t ring_lds(const nc_gpuhash_ring_t *r)
 {
     return ((4u * (r->max_keys + 1u) + 15u) & ~(size_t)15u) + r->kstride + 96u;
@@ -427,8 +475,9 @@ static rstatus_t ring_ensure_worker(nc_gpuhash_ring_t *r, uint32_t g)
     (void)hipGetLastError();
     r->epoch++;
     hipLaunchKernelGGL(ring_kernel(r->threads), dim3(r->nlanes), dim3(r->threads), ring_lds(r), r->stream, r->d_ctl,
-                       r->dv, r->d_desc, r->d_done, r->d_offs, r->d_keys, r->d_outs, r->nslots, r->max_keys,
-                       r->kstride, r->nlanes, r->epoch, r->timeline ? r->d_tl : nullptr);
+                       r->dv, r->d_stopw, r->stop_stride, r->d_desc, r->d_done, r->d_offs, r->d_keys, r->d_outs,
+                       r->nslots, r->max_keys, r->kstride, r->nlanes, r->epoch, r->flags,
+                       r->timeline ? r->d_tl : nullptr);
     e = hipGetLastError();
     if (e == hipSuccess) e = hipEventRecord(r->ev, r->stream);
     if (e != hipSuccess) return ring_fail(e);
@@ -441,12 +490,17 @@ extern "C" void nc_gpuhash_ring_destroy(nc_gpuhash_ring_t *r)
 {
     if (r == NULL) return;
     for (uint32_t g = 0; g < kMaxLanes && r->ctl != NULL; g++) __atomic_store_n(&r->ctl[g].stop, 1u, __ATOMIC_SEQ_CST);
+    if (r->stage != NULL && r->stopw != NULL) { /* through the BAR: a plain store, then a fence that drains it */
+        __atomic_store_n(r->stopw, 1u, __ATOMIC_RELEASE);
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    }
     (void)hipSetDevice(r->device);
     if (r->launched) (void)hipEventSynchronize(r->ev); /* every lane returns at its next poll */
     if (r->ev) (void)hipEventDestroy(r->ev);
     if (r->stream) (void)hipStreamDestroy(r->stream);
     if (r->dv) (void)hipFree(r->dv);
     if (r->host) (void)hipHostFree(r->host);
+    if (r->stage) (void)hipFree(r->stage);
     free(r->slot_state);
     free(r->slot_seq);
     free(r->slot_nkeys);
@@ -486,13 +540,31 @@ extern "C" nc_gpuhash_ring_t *nc_gpuhash_ring_create_ex(int device, uint32_t nsl
     r->slot_seq = (uint64_t *)calloc(nslots, sizeof(uint64_t));
     r->slot_nkeys = (uint32_t *)calloc(nslots, sizeof(uint32_t));
     r->slot_out = (uint32_t **)calloc(nslots, sizeof(uint32_t *));
-    const size_t o_ctl = 0, o_desc = sizeof(RingCtl) * kMaxLanes, o_done = o_desc + 8u * nslots,
-                 o_offs = (o_done + 4u * nslots + 127u) & ~(size_t)127u,
+    /* host-written words (stop, desc, offsets, keys) from o_stop to o_done,
+     * device-written ones (ctl's device half, done, outputs, timeline) around
+     * them; with device staging the host-written block is the stage */
+    const size_t o_ctl = 0, o_stop = sizeof(RingCtl) * kMaxLanes, o_desc = o_stop + 128u,
+                 o_offs = (o_desc + 8u * nslots + 127u) & ~(size_t)127u,
                  o_keys = (o_offs + 4ull * max_keys * nslots + 127u) & ~(size_t)127u,
-                 o_outs = o_keys + r->kstride * nslots, o_tl = (o_outs + 4ull * max_keys * nslots + 127u) & ~(size_t)127u,
+                 o_done = o_keys + r->kstride * nslots, o_outs = (o_done + 4u * nslots + 127u) & ~(size_t)127u,
+                 o_tl = (o_outs + 4ull * ((max_keys + 3u) & ~3u) * nslots + 127u) & ~(size_t)127u,
                  total = o_tl + 64ull * nslots;
     hipError_t e = r->slot_state && r->slot_seq && r->slot_nkeys && r->slot_out ? hipSetDevice(device)
                                                                                 : hipErrorOutOfMemory;
+    int large_bar = 0;
+    const char *sv = getenv("NC_GPUHASH_RING_STAGING"), *wv = getenv("NC_GPUHASH_RING_WT");
+    r->flags = (wv != NULL && strcmp(wv, "0") == 0) ? 0u : 1u; /* A/B: NC_GPUHASH_RING_WT=0, plain stores + release */
+    const int want_dev = sv != NULL ? strcmp(sv, "device") == 0 : r->nlanes <= 2u;
+    if (e == hipSuccess && want_dev &&
+        hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) == hipSuccess && large_bar) {
+        /* the host stores into it through the BAR; nothing else falls back on failure */
+        if (hipExtMallocWithFlags((void **)&r->stage, o_done - o_stop, hipDeviceMallocUncached) != hipSuccess) {
+            (void)hipGetLastError();
+            r->stage = NULL;
+        } else if (hipMemset(r->stage, 0, o_done - o_stop) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            e = hipErrorUnknown;
+        }
+    }
     if (e == hipSuccess) e = hipHostMalloc((void **)&r->host, total, hipHostMallocMapped | hipHostMallocCoherent);
     uint8_t *dev = NULL;
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&dev, r->host, 0);
@@ -510,19 +582,31 @@ extern "C" nc_gpuhash_ring_t *nc_gpuhash_ring_create_ex(int device, uint32_t nsl
     }
     memset(r->host, 0, total);
     r->ctl = (RingCtl *)(r->host + o_ctl);
-    r->desc = (uint64_t *)(r->host + o_desc);
     r->done = (uint32_t *)(r->host + o_done);
-    r->offs = (uint32_t *)(r->host + o_offs);
-    r->keys = r->host + o_keys;
     r->outs = (uint32_t *)(r->host + o_outs);
     r->tl = (uint64_t *)(r->host + o_tl);
     r->d_tl = (uint64_t *)(dev + o_tl);
     r->d_ctl = (RingCtl *)(dev + o_ctl);
-    r->d_desc = (uint64_t *)(dev + o_desc);
     r->d_done = (uint32_t *)(dev + o_done);
-    r->d_offs = (uint32_t *)(dev + o_offs);
-    r->d_keys = dev + o_keys;
     r->d_outs = (uint32_t *)(dev + o_outs);
+    /* the host-written block: the stage (one address for host and device,
+     * the BAR mapping) or the host allocation's own */
+    uint8_t *hw = r->stage ? r->stage - o_stop : r->host, *dw = r->stage ? r->stage - o_stop : dev;
+    r->desc = (uint64_t *)(hw + o_desc);
+    r->offs = (uint32_t *)(hw + o_offs);
+    r->keys = hw + o_keys;
+    r->d_desc = (uint64_t *)(dw + o_desc);
+    r->d_offs = (uint32_t *)(dw + o_offs);
+    r->d_keys = dw + o_keys;
+    if (r->stage) { /* one stop word for every lane */
+        r->stopw = (uint32_t *)r->stage;
+        r->d_stopw = (uint32_t *)r->stage;
+        r->stop_stride = 0;
+    } else {
+        r->stopw = &r->ctl[0].stop;
+        r->d_stopw = &r->d_ctl[0].stop;
+        r->stop_stride = sizeof(RingCtl) / sizeof(uint32_t);
+    }
     return r;
 }
 
@@ -538,7 +622,7 @@ static int ring_reap(nc_gpuhash_ring_t *r, uint32_t s)
     if (r->slot_state[s] == SLOT_FREE) return 1;
     if (__atomic_load_n(&r->done[s], __ATOMIC_ACQUIRE) != ring_tag(r->slot_seq[s])) return 0;
     if (r->slot_out[s] != NULL) /* NULL: the ticket was forgotten (its owner is gone) */
-        memcpy(r->slot_out[s], r->outs + (size_t)s * r->max_keys, (size_t)r->slot_nkeys[s] * sizeof(uint32_t));
+        memcpy(r->slot_out[s], r->outs + (size_t)s * ((r->max_keys + 3u) & ~3u), (size_t)r->slot_nkeys[s] * sizeof(uint32_t));
     r->slot_state[s] = SLOT_FREE;
     return 1;
 }
@@ -610,9 +694,14 @@ extern "C" rstatus_t nc_gpuhash_ring_submit_spans(nc_gpuhash_ring_t *r, int mode
     r->slot_nkeys[s] = nkeys;
     r->slot_out[s] = out;
     r->seq = seq + 1u;
-    /* every staging write before the descriptor; then `exiting`
-     * (ring_ensure_worker) after it: the host's half of the leave protocol */
-    __atomic_store_n(&r->desc[s], desc_pack(ring_tag(seq), (uint32_t)mode, nkeys, (uint32_t)pos), __ATOMIC_SEQ_CST);
+    /* every staging write before the descriptor, then `exiting`
+     * (ring_ensure_worker) after it: the host's half of the leave protocol.
+     * Two full fences around a plain 64-bit store, no locked instruction:
+     * with device staging the stores are write-combined through the BAR (a
+     * locked read-modify-write has no business on PCIe), and the fences drain
+     * the write-combining buffers in order */
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    __atomic_store_n(&r->desc[s], desc_pack(ring_tag(seq), (uint32_t)mode, nkeys, (uint32_t)pos), __ATOMIC_RELEASE);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
     const rstatus_t rc = ring_ensure_worker(r, g);
     if (rc == NC_OK) *ticket = (int)(seq & kTagMask);
@@ -725,6 +814,8 @@ extern "C" rstatus_t nc_gpuhash_ring_debug_hold(nc_gpuhash_ring_t *r, int hold)
 }
 
 extern "C" uint32_t nc_gpuhash_ring_lanes(const nc_gpuhash_ring_t *r) { return r ? r->nlanes : 0; }
+
+extern "C" int nc_gpuhash_ring_debug_staging(const nc_gpuhash_ring_t *r) { return r ? (r->stage != NULL) : -1; }
 
 extern "C" rstatus_t nc_gpuhash_ring_limits(const nc_gpuhash_ring_t *r, uint32_t *max_keys, uint64_t *max_key_bytes,
                                             uint32_t *nslots)

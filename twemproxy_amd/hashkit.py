@@ -553,6 +553,12 @@ class Ring:
     def lanes(self) -> int:
         return int(self._lib.nc_gpuhash_ring_lanes(self._h))
 
+    @property
+    def staging(self) -> str:
+        """where batches are staged: "device" (HBM written through the PCIe
+        BAR) or "host" (mapped host memory)"""
+        return "device" if self._lib.nc_gpuhash_ring_debug_staging(self._h) == 1 else "host"
+
     def debug_start_seq(self, seq: int) -> None:
         """number this (fresh) ring's batches from `seq` (tests of the ticket wrap)"""
         L.check(self._lib.nc_gpuhash_ring_debug_start_seq(self._h, seq), "nc_gpuhash_ring_debug_start_seq")
