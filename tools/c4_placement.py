@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--spacer-gib", type=int, default=0, help="hold this much device memory before synthesising the keys")
     ap.add_argument("--contig-only", action="store_true",
                     help="only the synthesised keys and a copy in hipExtMallocWithFlags(hipDeviceMallocContiguous) memory")
+    ap.add_argument("--grid", action="store_true", help="4 key placements x 4 offset placements")
+    ap.add_argument("--keys-only", action="store_true", help="with --grid: the 4 key placements, one offsets buffer "
+                    "(for a PMC pass: 4 checks, then per placement 3 warm-up + ITERS timed launches, in order)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -69,6 +72,38 @@ def main():
                           "ms_min": {k: round(min(v), 4) for k, v in res.items()},
                           "ptr_hex": {"synth": hex(keys.data_ptr()), "contiguous": hex(p.value)}}), flush=True)
         hip.hipFree(p)
+        return
+    if args.grid:
+        # keys x offsets placements: which of the two buffers (or the pair)
+        # decides the mode
+        kp = {"k0": keys}
+        op = {"o0": off}
+        for i in (1, 2, 3):
+            b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+            b.copy_(keys)
+            kp[f"k{i}"] = b
+            if args.keys_only:
+                continue
+            o = torch.empty(off.numel() + (i << 14), dtype=off.dtype, device="cuda")[i << 14:]
+            o.copy_(off)
+            op[f"o{i}"] = o
+        torch.cuda.synchronize()
+        res, chk = {}, {}
+        for kn, k in kp.items():
+            for on, o in op.items():
+                got = t.hash_batch_device(args.mode, k, o, shape=shape, key_end=kb).cpu().numpy()
+                chk[f"{kn}{on}"] = "ok" if np.array_equal(got, ref) else "DIFF"
+                res[f"{kn}{on}"] = []
+        for _ in range(args.rounds):
+            for kn, k in kp.items():
+                for on, o in op.items():
+                    t.time_batch_device(args.mode, k, o, out, 3, shape=shape)
+                    res[f"{kn}{on}"].append(t.time_batch_device(args.mode, k, o, out, args.iters, shape=shape))
+        print(json.dumps({"mode": args.mode, "config": "C4S", "grid": "keys k0-k3 x offsets o0-o3",
+                          "ms_median": {k: round(statistics.median(v), 4) for k, v in res.items()},
+                          "check": "ok" if all(v == "ok" for v in chk.values()) else chk,
+                          "keys_ptr": {k: hex(v.data_ptr()) for k, v in kp.items()},
+                          "offs_ptr": {k: hex(v.data_ptr()) for k, v in op.items()}}), flush=True)
         return
     fresh = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     fresh.copy_(keys)
