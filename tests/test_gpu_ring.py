@@ -216,6 +216,43 @@ def test_ring_tiny_batches(gpu, oracle, lanes):
             np.testing.assert_array_equal(out, w, err_msg=f"{t.HASH_NAMES[m]} {len(spans)}")
 
 
+def test_ring_create_while_another_runs(gpu, oracle):
+    """a ring created while another ring's resident worker serves a steady
+    stream neither waits for that worker (its set-up synchronises only its
+    own stream) nor disturbs it"""
+    rng = np.random.default_rng(91)
+    buf, spans = batch(rng, 300, maxlen=60)
+    w = want(oracle, 6, buf, spans)
+    stop = threading.Event()
+    errors, served = [], [0]
+    with t.Ring(0, nslots=2, lanes=1) as a:
+        def feed():
+            try:
+                while not stop.is_set():
+                    tk, out = a.submit_spans(6, buf, spans)
+                    a.wait(tk)
+                    np.testing.assert_array_equal(out, w)
+                    served[0] += 1
+            except Exception as e:  # noqa: BLE001 - reported below
+                errors.append(e)
+        th = threading.Thread(target=feed)
+        th.start()
+        try:
+            time.sleep(0.2)  # the worker is resident and busy
+            t0 = time.perf_counter()
+            with t.Ring(0, nslots=2, lanes=1) as b:
+                took = time.perf_counter() - t0
+                tk, out = b.submit_spans(6, buf, spans)
+                b.wait(tk)
+                np.testing.assert_array_equal(out, w)
+        finally:
+            stop.set()
+            th.join(30)
+    assert not errors, errors[0]
+    assert served[0] > 100
+    assert took < 0.5, f"ring create took {took:.3f} s beside a running worker"
+
+
 def test_ring_rejects_spans_outside_the_buffer(gpu):
     with t.Ring(0, nslots=2) as r:
         buf = np.zeros(100, np.uint8)

@@ -555,23 +555,26 @@ extern "C" nc_gpuhash_ring_t *nc_gpuhash_ring_create_ex(int device, uint32_t nsl
     const char *sv = getenv("NC_GPUHASH_RING_STAGING"), *wv = getenv("NC_GPUHASH_RING_WT");
     r->flags = (wv != NULL && strcmp(wv, "0") == 0) ? 0u : 1u; /* A/B: NC_GPUHASH_RING_WT=0, plain stores + release */
     const int want_dev = sv != NULL ? strcmp(sv, "device") == 0 : r->nlanes <= 2u;
-    if (e == hipSuccess && want_dev &&
-        hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) == hipSuccess && large_bar) {
-        /* the host stores into it through the BAR; nothing else falls back on failure */
-        if (hipExtMallocWithFlags((void **)&r->stage, o_done - o_stop, hipDeviceMallocUncached) != hipSuccess) {
-            (void)hipGetLastError();
-            r->stage = NULL;
-        } else if (hipMemset(r->stage, 0, o_done - o_stop) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-            e = hipErrorUnknown;
-        }
-    }
     if (e == hipSuccess) e = hipHostMalloc((void **)&r->host, total, hipHostMallocMapped | hipHostMallocCoherent);
     uint8_t *dev = NULL;
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&dev, r->host, 0);
     if (e == hipSuccess) e = hipMalloc((void **)&r->dv, sizeof(RingDev));
-    if (e == hipSuccess) e = hipMemset(r->dv, 0, sizeof(RingDev));
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev, hipEventDisableTiming);
+    /* zeroed on the ring's own stream: a device-wide synchronize would wait
+     * for another ring's resident worker */
+    if (e == hipSuccess) e = hipMemsetAsync(r->dv, 0, sizeof(RingDev), r->stream);
+    if (e == hipSuccess && want_dev &&
+        hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) == hipSuccess && large_bar) {
+        /* the host stores into it through the BAR; if it cannot be had, host staging */
+        if (hipExtMallocWithFlags((void **)&r->stage, o_done - o_stop, hipDeviceMallocUncached) != hipSuccess) {
+            (void)hipGetLastError();
+            r->stage = NULL;
+        } else {
+            e = hipMemsetAsync(r->stage, 0, o_done - o_stop, r->stream);
+        }
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
     if (e == hipSuccess && ring_lds(r) > 64u * 1024u) e = hipErrorInvalidValue;
     if (e != hipSuccess) {
         ring_fail(e);
