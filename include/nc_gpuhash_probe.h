@@ -41,8 +41,9 @@ rstatus_t nc_gpuhash_probe_mix(const void *d_buf, uint64_t bytes, void *d_wout, 
  * with nt 16-byte loads by 512-thread workgroups (`grid` of them, tiles
  * grid-strided in runs of `run` consecutive tiles), each tile's tile_write
  * output bytes at d_out + tile * tile_write — stored after its tile, or
- * (defer) once per run from LDS, run * tile_write <= 8 KiB contiguous.
- * Mean ms per pass of all bytes / tile_read tiles. */
+ * (defer bit 0) once per run from LDS, run * tile_write <= 8 KiB contiguous;
+ * defer bits 4-5 the stores' flavour: 0 nt, 1 plain, 2 sc1, 3 sc0 sc1 (2 and 3
+ * need out_bytes < 2 GiB). Mean ms per pass of all bytes / tile_read tiles. */
 rstatus_t nc_gpuhash_probe_tile_mix(const void *d_buf, uint64_t bytes, void *d_out, uint64_t out_bytes,
                                    uint32_t tile_read, uint32_t tile_write, uint32_t run, uint32_t grid, int defer,
                                    uint32_t *d_sink, void *stream, int iters, float *avg_ms);

@@ -111,8 +111,23 @@ rstatus_t probe_read(const void *d_buf, uint64_t bytes, uint32_t *d_sink, void *
  * stored right after the tile (DEFER = false: 2 KiB pieces, the kernel's
  * coalesced store) or held in LDS and stored once per run (DEFER = true:
  * run * wr contiguous bytes at once). rd a multiple of 8 KiB, wr of 16 and
- * at most 8 KiB / run. */
-template <bool DEFER>
+ * at most 8 KiB / run. SF: the output stores' flavour — 0 nt (the
+ * kernels'), 1 plain, 2 sc1, 3 sc0 sc1 (write-through). */
+template <int SF>
+__device__ __forceinline__ void tile_mix_store(uint32_t __attribute__((ext_vector_type(4))) y, uint4 *out, uint64_t q)
+{
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    if constexpr (SF == 0) {
+        __builtin_nontemporal_store(y, reinterpret_cast<v4u *>(out) + q);
+    } else if constexpr (SF == 1) {
+        reinterpret_cast<v4u *>(out)[q] = y;
+    } else { /* a buffer store, 16 B a lane, over the uniform base (offsets < 4 GiB: the probe's outputs) */
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(y, r, (int)(q * 16u), 0, SF == 2 ? 16 : 17);
+    }
+}
+
+template <bool DEFER, int SF>
 __global__ __launch_bounds__(512) void probe_tile_mix_kernel(const uint4 *__restrict__ in, uint64_t ntiles, uint32_t rd,
                                                              uint32_t wr, uint32_t run, uint4 *__restrict__ out,
                                                              uint32_t *__restrict__ sink)
@@ -140,7 +155,7 @@ __global__ __launch_bounds__(512) void probe_tile_mix_kernel(const uint4 *__rest
             if constexpr (DEFER) {
                 if (t < wq) stage[k * wq + t] = make_uint4(y.x, y.y, y.z, y.w);
             } else {
-                if (t < wq) __builtin_nontemporal_store(y, reinterpret_cast<v4u *>(out) + tile * wq + t);
+                if (t < wq) tile_mix_store<SF>(y, out, tile * wq + t);
             }
             acc ^= y.x;
         }
@@ -150,7 +165,7 @@ __global__ __launch_bounds__(512) void probe_tile_mix_kernel(const uint4 *__rest
             for (uint32_t i = t; i < n; i += 512u) {
                 const uint4 z = stage[i];
                 const v4u y = {z.x, z.y, z.z, z.w};
-                __builtin_nontemporal_store(y, reinterpret_cast<v4u *>(out) + r0 * wq + i);
+                tile_mix_store<SF>(y, out, r0 * wq + i);
             }
             __syncthreads();
         }
@@ -208,12 +223,18 @@ extern "C" rstatus_t nc_gpuhash_probe_tile_mix(const void *d_buf, uint64_t bytes
         return NC_ERROR;
     }
     const uint64_t ntiles = bytes / tile_read;
-    if (ntiles * tile_write > out_bytes) {
+    if (ntiles * tile_write > out_bytes || (((defer >> 4) & 3) >= 2 && out_bytes > 0x7fffffffull)) {
         errno = EINVAL;
         return NC_ERROR;
     }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    auto k = defer ? probe_tile_mix_kernel<true> : probe_tile_mix_kernel<false>;
+    typedef void (*mix_fn)(const uint4 *, uint64_t, uint32_t, uint32_t, uint32_t, uint4 *, uint32_t *);
+    static const mix_fn kinds[2][4] = {
+        {probe_tile_mix_kernel<false, 0>, probe_tile_mix_kernel<false, 1>, probe_tile_mix_kernel<false, 2>,
+         probe_tile_mix_kernel<false, 3>},
+        {probe_tile_mix_kernel<true, 0>, probe_tile_mix_kernel<true, 1>, probe_tile_mix_kernel<true, 2>,
+         probe_tile_mix_kernel<true, 3>}};
+    const mix_fn k = kinds[(defer & 1) != 0][(defer >> 4) & 3];
     hipEvent_t a, b;
     if (hipEventCreate(&a) != hipSuccess) {
         errno = ENODEV;
