@@ -18,6 +18,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
@@ -43,6 +44,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--nkeys", type=int, default=1 << 26)
+    ap.add_argument("--spinup", type=float, default=0.0, help="seconds of untimed launches before each timing")
     ap.add_argument("--lib", default="", help="another build of libnc_gpuhash.so (same-box A/B of builds)")
     args = ap.parse_args()
 
@@ -88,6 +90,10 @@ def main():
                 else:
                     diff = np.flatnonzero(h != ref)
                     ok[v] = "same" if diff.size == 0 else f"DIFF {diff.size} first {int(diff[0])}"
+            if args.spinup > 0:  # clocks ramp up under load (bench.py SPINUP_S): untimed launches first
+                t_end = time.perf_counter() + args.spinup
+                while time.perf_counter() < t_end:
+                    t.time_batch_device(mode, keys, off, out, 10, shape=shape)
             for _ in range(args.rounds):
                 for v in variants:
                     L.lib().nc_gpuhash_set_tuning(tune[v][0], 0, tune[v][1])

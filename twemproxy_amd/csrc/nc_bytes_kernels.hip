@@ -20,6 +20,7 @@
 
 #include "nc_crc_slice.h"
 #include "nc_direct.h"
+#include "nc_out_policy.h"
 #include "nc_gpuhash.h"
 #include "nc_hash_algo.h"
 #include "nc_hash_key.h"
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_direct_kernel(const uint8
             }
             if (rem <= (int32_t)RB) {
                 const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
-                __builtin_amdgcn_raw_buffer_store_b32(final_state<MODE>(h), rout, (int)(lane * 4u), 0, kAuxNt);
+                __builtin_amdgcn_raw_buffer_store_b32(final_state<MODE>(h), rout, (int)(lane * 4u), 0, kAuxOut);
             }
         }
         if (more) {
@@ -506,7 +507,7 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_short_kernel(const uint8_
                 hv = final_state<MODE>(short_step<MODE, NC, NW, R>(init_state<MODE>(), dat[q], (int32_t)len, tab, lane4));
             }
             const rsrc_t rout = make_rsrc(out + k0, 4u * nv); /* lanes past the batch: dropped */
-            __builtin_amdgcn_raw_buffer_store_b32(hv, rout, (int)(lane * 4u), 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(hv, rout, (int)(lane * 4u), 0, kAuxOut);
         }
     }
     /* tiles jbad .. n - 1 (only when a key was longer than the shape said),
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_short_kernel(const uint8_
         if constexpr (is_word_mode<MODE>()) { /* byte loads, one lane per key (nc_hash_key.h) */
             const uint32_t hw = lane < nv ? nc_key_hash(MODE, keys + s0 + vo, (uint64_t)rem, nullptr, nullptr) : 0u;
             const rsrc_t rw = make_rsrc(out + k0, 4u * nv);
-            __builtin_amdgcn_raw_buffer_store_b32(hw, rw, (int)(lane * 4u), 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(hw, rw, (int)(lane * 4u), 0, kAuxOut);
             continue;
         }
         uint32_t h = init_state<MODE>();
@@ -544,7 +545,7 @@ __global__ __launch_bounds__(64 * WAVES) void nc_bytes_short_kernel(const uint8_
             rem -= 64;
         }
         const rsrc_t rout = make_rsrc(out + k0, 4u * nv);
-        __builtin_amdgcn_raw_buffer_store_b32(final_state<MODE>(h), rout, (int)(lane * 4u), 0, kAuxNt);
+        __builtin_amdgcn_raw_buffer_store_b32(final_state<MODE>(h), rout, (int)(lane * 4u), 0, kAuxOut);
     }
 }
 

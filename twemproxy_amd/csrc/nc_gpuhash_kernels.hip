@@ -31,6 +31,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include "nc_out_policy.h"
 #include "nc_gpuhash.h"
 #include "nc_gpuhash_probe.h"
 #include "nc_hash_algo.h"
@@ -593,7 +594,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<MODE>()) void nc_hash_kernel(cons
             full_barrier();
         }
         if (pend_idx != ~0ull) {
-            if constexpr (kNT) __builtin_nontemporal_store(pend_h, out + pend_idx);
+            if constexpr (kNT) out_st32(out + pend_idx, pend_h);
             else out[pend_idx] = pend_h;
         }
         pend_idx = ~0ull;
@@ -1031,12 +1032,14 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
                 const uint32_t q = 64u * (wave - 1u) + lane; /* 16-byte piece */
                 gs_u32x4 v;
                 asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ra + 16u * q) : "memory");
-                __builtin_nontemporal_store(v, reinterpret_cast<gs_u32x4 *>(dst) + q);
+                if constexpr (NC_OUT_POLICY == 0) __builtin_nontemporal_store(v, reinterpret_cast<gs_u32x4 *>(dst) + q);
+                else __builtin_amdgcn_raw_buffer_store_b128(
+                    v, __builtin_amdgcn_make_buffer_rsrc(dst, 0, 4 * TK, 0x00020000), (int)(16u * q), 0, kAuxOut);
             }
         } else if (t < pend_cnt) {
             uint32_t v;
             asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ra + 4u * t) : "memory");
-            __builtin_nontemporal_store(v, dst + t);
+            out_st32(dst + t, v);
         }
     };
     for (uint32_t it = 0;; it++) {
@@ -1047,7 +1050,7 @@ __device__ __forceinline__ void gs_body(const uint8_t *__restrict__ keys_base, c
         if constexpr (CS && !kIssueFirst) {
             if (pend_tile != ~0ull) store_tile();
         } else if constexpr (!CS) {
-            if (pend_idx != ~0ull) __builtin_nontemporal_store(pend_h, out + pend_idx);
+            if (pend_idx != ~0ull) out_st32(out + pend_idx, pend_h);
             pend_idx = ~0ull;
         }
         asm volatile("" ::: "memory");
@@ -1248,7 +1251,7 @@ __device__ __forceinline__ u32x4_t asm_ld128(const void *p)
 template <bool NT = false>
 __device__ __forceinline__ void asm_st32(void *p, uint32_t v)
 {
-    if constexpr (NT) asm volatile("global_store_dword %0, %1, off nt" : : "v"(p), "v"(v) : "memory");
+    if constexpr (NT) out_asm_st32(p, v); /* the hash outputs' policy (nc_out_policy.h) */
     else asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
 }
 

@@ -44,6 +44,7 @@
 #include "nc_hash_algo.h"
 #include "nc_md5_steps.h"
 #include "nc_direct.h"
+#include "nc_out_policy.h"
 
 namespace {
 
@@ -102,7 +103,7 @@ __device__ __forceinline__ void tail_entry(const uint32_t *qw, uint32_t slot, ui
     w[14] = len << 3;
     w[15] = len >> 29;
     /* words 1..13 are zero: folded into the steps' constants */
-    __builtin_nontemporal_store(md5_tail_final_a(st, w), out + idx);
+    out_st32(out + idx, md5_tail_final_a(st, w));
 }
 
 __device__ __forceinline__ void run_tail(Queue &q, uint32_t lane, uint32_t *__restrict__ out)
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                     uint32_t v[4] = {NC_MD5_A0, NC_MD5_B0, NC_MD5_C0, NC_MD5_D0};
                     md5_steps_fl<FL>(v, w, std::make_integer_sequence<int, 61>{});
                     const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
-                    __builtin_amdgcn_raw_buffer_store_b32(NC_MD5_A0 + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
+                    __builtin_amdgcn_raw_buffer_store_b32(NC_MD5_A0 + v[0], rout, (int)(lane * 4u), 0, kAuxOut);
                 }
             }
         }
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(256, 8) void nc_md5_direct_kernel(const uint8_t *__
                 if (FS ? rem <= 64 : fin) {
                     const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
                     __builtin_amdgcn_raw_buffer_store_b32((FIRST ? NC_MD5_A0 : st[0]) + v[0], rout, (int)(lane * 4u),
-                                                          0, kAuxNt);
+                                                          0, kAuxOut);
                 }
                 if (fin || S) { /* (S: a key of 56..64 bytes queues its tail block) */
                 } else if (len - 56u > 8u) {
@@ -467,7 +468,7 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
         md5_steps(v, w, std::make_integer_sequence<int, 61>{});
         if (fin) {
             const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
-            __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(st[0] + v[0], rout, (int)(lane * 4u), 0, kAuxOut);
         } else {
             md5_steps_from61(v, w, std::make_integer_sequence<int, 3>{});
             st[0] += v[0];
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(256) void nc_md5_lines_kernel(const uint8_t *__rest
             w[14] = cur_t.len << 3;
             w[15] = cur_t.len >> 29;
             const rsrc_t rout = make_rsrc(out + wk.key0(tile), 256u);
-            __builtin_amdgcn_raw_buffer_store_b32(md5_tail_final_a(st, w), rout, (int)(lane * 4u), 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(md5_tail_final_a(st, w), rout, (int)(lane * 4u), 0, kAuxOut);
         }
         if (more) {
             b++;

@@ -26,6 +26,7 @@
 #include <stdint.h>
 
 #include "nc_direct.h"
+#include "nc_out_policy.h"
 #include "nc_gpuhash.h"
 #include "nc_hash_algo.h"
 #include "nc_sorted_hash.h"
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
         const rsrc_t rout = make_rsrc(out + k0, (uint64_t)nv * 4u); /* keys past nkeys: dropped */
 #pragma unroll
         for (int q = 0; q < 4; q++)
-            __builtin_amdgcn_raw_buffer_store_b32(hq[q], rout, (int)(4u * ((kq >> (8 * q)) & 0xffu)), 0, kAuxNt);
+            __builtin_amdgcn_raw_buffer_store_b32(hq[q], rout, (int)(4u * ((kq >> (8 * q)) & 0xffu)), 0, kAuxOut);
     };
 
     for (uint64_t t = 0; t < n; t++) {
