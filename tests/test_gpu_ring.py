@@ -7,7 +7,9 @@ across 2^31 and 2^32 batches, and the limits. Every test runs twice: with the
 batches staged in device memory written through the PCIe BAR
 (NC_GPUHASH_RING_STAGING=device; the default for rings of 1 or 2 lanes on a
 large-BAR device such as the MI355X) and in mapped host memory
-(NC_GPUHASH_RING_STAGING=host; the default for 4 lanes and more)."""
+(NC_GPUHASH_RING_STAGING=host; the default for 4 lanes and more), and a
+third time with device staging and the hashes published by a release
+instead of stored write-through (NC_GPUHASH_RING_WT=0)."""
 import ctypes
 import threading
 import time
@@ -20,11 +22,19 @@ import twemproxy_amd as t
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(120)]
 
 
-@pytest.fixture(autouse=True, params=["device", "host"])
+@pytest.fixture(autouse=True, params=["device", "host", "device-release"])
 def staging(request, monkeypatch):
-    """the staging every ring of the test is created with (read at create)"""
-    monkeypatch.setenv("NC_GPUHASH_RING_STAGING", request.param)
-    return request.param
+    """the staging every ring of the test is created with (read at create);
+    "device-release": device staging with the hashes stored plainly and
+    published by a system-scope release (NC_GPUHASH_RING_WT=0, the A/B of the
+    default write-through stores)"""
+    st = request.param.split("-")[0]
+    monkeypatch.setenv("NC_GPUHASH_RING_STAGING", st)
+    if request.param.endswith("-release"):
+        monkeypatch.setenv("NC_GPUHASH_RING_WT", "0")
+    else:
+        monkeypatch.delenv("NC_GPUHASH_RING_WT", raising=False)
+    return st
 
 
 def test_ring_staging_is_the_one_asked_for(gpu, staging):
