@@ -23,8 +23,9 @@ RUNS = [
                   "host staging with wt1"),
     ("r06zd_acq", "DROPPED: sc0 sc1 fetch loads with no acquire fence (acq0) against the acquire (acq1), "
                   "alternated twice on one box: no difference (a box slow at BAR stores and uncached reads)"),
-    ("r06ze_pairs", "the final ring: device staging (default for one lane) against host staging, alternated "
-                    "twice on one box"),
+    ("r06ze_pairs", "device staging (default for one lane) against host staging, alternated twice on one box"),
+    ("r06zm_copy", "KEPT: the staging copy into BAR memory as 64-byte AVX-512 stores (default) against 32-byte "
+                   "AVX2 stores and glibc memcpy, alternated twice on one box"),
 ]
 
 
