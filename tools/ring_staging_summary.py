@@ -33,9 +33,10 @@ def main():
     out = {"what": "the batch ring at small depth (DESIGN.md §6.2.1): tools/gpu_r6_bar.sh, one fresh MI355X box "
                    "per run; rows from tools/nc_c5_replay (1024-thread lanes, depth <= 8)",
            "runs": []}
-    probe = "gpurun_out/bar_probe2.jsonl"
-    if os.path.exists(probe):
-        out["bar_probe"] = [json.loads(l) for l in open(probe) if l.startswith("{")]
+    out["bar_probe"] = []
+    for probe in ("gpurun_out/bar_probe2.jsonl", "gpurun_out/bar_probe3.jsonl"):  # attributes + ping-pong; copies
+        if os.path.exists(probe):
+            out["bar_probe"] += [json.loads(l) for l in open(probe) if l.startswith("{")]
     for name, what in RUNS:
         d = f"gpurun_out/{name}"
         if not os.path.isdir(d):
