@@ -30,21 +30,25 @@
  *     poll; the acquire fence only once the descriptor matches); the load
  *     that finds the slot published also carries the batch's shape. The
  *     workgroup stages the slot's spans and key bytes into LDS with
- *     coalesced 16-byte reads across PCIe, all in flight at once, every
- *     thread hashes keys from LDS with the batch kernels' realigning word
- *     readers (nc_lds_hash.h: aligned dwords + v_alignbyte, reads a step
- *     ahead, all 12 modes; byte-at-a-time LDS reads would put one LDS
- *     latency on every key byte), writes the hashes to the slot's mapped
- *     output, and
- *     thread 0 issues one system-scope release and the slot's done word.
+ *     coalesced 16-byte reads (across PCIe, or from HBM with device
+ *     staging), all in flight at once, every thread hashes keys from LDS
+ *     with the batch kernels' realigning word readers (nc_lds_hash.h:
+ *     aligned dwords + v_alignbyte, reads a step ahead, all 12 modes;
+ *     byte-at-a-time LDS reads would put one LDS latency on every key
+ *     byte) and leaves each hash in LDS; the hashes go to the slot's mapped
+ *     output as 16-byte write-through stores (sc0 sc1), every storing wave
+ *     drains them, and after a barrier thread 0 stores the slot's done word
+ *     — no system-scope release (NC_GPUHASH_RING_WT=0: plain stores and the
+ *     release, the A/B).
  *   host poll: one load of that word; the hashes are copied to the caller.
  *
  * Staging in device memory: where the host can store into the device's HBM
  * through the PCIe BAR (a large-BAR device, hipDeviceAttributeIsLargeBar),
  * the host-written, device-read words — descriptors, key spans, key images
  * and the `stop` word — live in ONE uncached device allocation instead: the
- * host's memcpy crosses PCIe as posted writes (write-combined, ~0.8 us for a
- * C5 mbuf's 15.4 KB, tools/probes/bar_probe.hip), and the worker's poll and
+ * host's copy crosses PCIe as posted writes (write-combined: 0.41-0.58 us for
+ * a C5 mbuf's 15.4 KB by AVX stores, 0.58-0.8 by memcpy,
+ * tools/probes/bar_probe.hip), and the worker's poll and
  * fetch read HBM instead of crossing PCIe and back (the round trip of a flag
  * 1.75-2.1 us against 2.5-2.6 us in host memory, the same probe). Uncached:
  * the host rewrites a slot between batches behind L2's back, so no read of
