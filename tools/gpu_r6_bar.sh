@@ -3,9 +3,10 @@
 # host staging, and write-through hashes against plain stores + release
 # (the acquire fence against sc0 sc1 fetch loads was r06zd): the ring and
 # batch-site tests (both stagings), then the C5 replay and the depth-1
-# timeline under each configuration (staging:write-through[:copy], copy =
-# memcpy|avx2|avx512 for the staging copy; repeated configs give a paired
-# comparison on one box).
+# timeline under each configuration (staging:write-through[:copy[:deep]],
+# copy = memcpy|avx2|avx512 for the staging copy, deep = 1 for the byte
+# readers two steps ahead; repeated configs give a paired comparison on one
+# box).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -14,11 +15,12 @@ timeout -k 10 300 python3 -u -m pytest -x -v --timeout 100 --timeout-method thre
     tests/test_gpu_ring.py tests/test_gpu_batch_site.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -4 $O/tests.log
 for cfg in ${CONFIGS:-default:1 host:1 default:1 host:1}; do
-    IFS=: read -r st wt cp <<< "$cfg"
+    IFS=: read -r st wt cp dp <<< "$cfg"
     if [ $st = default ]; then unset NC_GPUHASH_RING_STAGING; else export NC_GPUHASH_RING_STAGING=$st; fi
     export NC_GPUHASH_RING_WT=$wt
     if [ -n "${cp:-}" ]; then export NC_GPUHASH_RING_COPY=$cp; else unset NC_GPUHASH_RING_COPY; fi
-    n=$(( ${n:-0} + 1 )); tag=${st}_wt${wt}_${cp:-defcopy}_$n
+    if [ "${dp:-0}" = 1 ]; then export NC_GPUHASH_RING_DEEP=1; else unset NC_GPUHASH_RING_DEEP; fi
+    n=$(( ${n:-0} + 1 )); tag=${st}_wt${wt}_${cp:-defcopy}_deep${dp:-0}_$n
     timeout -k 10 120 tools/nc_c5_replay 1.5 timeline > $O/timeline_$tag.jsonl 2> $O/timeline_$tag.err || { cat $O/timeline_$tag.err; exit 1; }
     echo "$tag $(cat $O/timeline_$tag.jsonl)"
     timeout -k 10 120 tools/nc_c5_replay 0.4 > $O/c5_$tag.jsonl 2> $O/c5_$tag.err || { cat $O/c5_$tag.err; exit 1; }

@@ -26,6 +26,8 @@ RUNS = [
     ("r06ze_pairs", "device staging (default for one lane) against host staging, alternated twice on one box"),
     ("r06zm_copy", "KEPT: the staging copy into BAR memory as 64-byte AVX-512 stores (default) against 32-byte "
                    "AVX2 stores and glibc memcpy, alternated twice on one box"),
+    ("r06zo_deep", "DROPPED: the worker's byte readers two steps ahead (QStream kDeep, deep1) against one (deep0), "
+                   "alternated twice on one box: the hash phase stays 1.88 us"),
 ]
 
 
