@@ -285,6 +285,7 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
     bool last_taken = false; /* thread 0: the one batch a leaving lane serves was taken */
     bool expired = false;    /* thread 0: a batch finished past kLifeTicks */
     uint64_t t_found = 0, t_staged = 0, t_issued = 0; /* thread 0: the diagnostic timeline (tl) */
+    uint64_t c_staged = 0, c_issued = 0; /* thread 0: shader-clock cycles (s_memtime) at the same two points */
     for (;;) {
         if (t == 0u) {
             uint32_t go = 0, lo = 0;
@@ -331,7 +332,10 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
         for (uint32_t j = 0; j < sizeof(kv) / sizeof(kv[0]); j++)
             if (t + j * T < nq) reinterpret_cast<u32x4 *>(lkeys)[t + j * T] = kv[j];
         __syncthreads();
-        if (tl != nullptr && t == 0u) t_staged = ticks();
+        if (tl != nullptr && t == 0u) {
+            t_staged = ticks();
+            c_staged = __builtin_readcyclecounter();
+        }
         uint32_t *so_out = outs + (uint64_t)s * ostride;
         const LdsSrc src{reinterpret_cast<const uint32_t *>(lkeys)};
         switch (mode) {
@@ -355,7 +359,10 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
         }
         if (tl != nullptr) { /* diagnostics: every thread's hashes issued (stores not yet acknowledged) */
             __syncthreads();
-            if (t == 0u) t_issued = ticks();
+            if (t == 0u) {
+                t_issued = ticks();
+                c_issued = __builtin_readcyclecounter();
+            }
         }
         __builtin_amdgcn_s_waitcnt(0); /* this thread's hash stores acknowledged ... */
         __syncthreads();                /* ... in every wave ... */
@@ -366,6 +373,9 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
                 __hip_atomic_store(&tl[8 * s + 1], (uint64_t)(t_staged), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&tl[8 * s + 2], (uint64_t)(t_issued), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&tl[8 * s + 3], (uint64_t)(ticks()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                /* [6]: the shader clock over the hash phase, MHz (cycles per 10 ns tick x 100) */
+                __hip_atomic_store(&tl[8 * s + 6], t_issued > t_staged ? (c_issued - c_staged) * 100u / (t_issued - t_staged) : 0u,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             if (wt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* the hashes went through: acknowledged above */
             else release_sys();
