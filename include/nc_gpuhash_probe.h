@@ -116,7 +116,8 @@ rstatus_t nc_gpuhash_ring_debug_hold(nc_gpuhash_ring_t *r, int hold);
  * acknowledged, written before the done word; [4] hashes released (or, with
  * write-through hashes, drained) and [5] the lane's batch count, stored just
  * before the done word and possibly landing just after it; [6] the shader
- * clock over the hash phase ([1] to [2]) in MHz. on = -1 only reads
+ * clock over the hash phase ([1] to [2]) in MHz; [7] when thread 0's wave
+ * finished its own keys (s_memrealtime). on = -1 only reads
  * slot `slot`'s eight words into out (when out is not NULL). */
 rstatus_t nc_gpuhash_ring_debug_timeline(nc_gpuhash_ring_t *r, int on, uint32_t slot, uint64_t out[8]);
 /* where the ring stages its batches: 1 = device memory written through the

@@ -83,7 +83,7 @@ static int ring_timeline(double seconds, struct mbuf *mb, uint32_t nmb, uint32_t
     nc_gpuhash_ring_t *ring = nc_gpuhash_ring_create_ex(0, 1, maxk, MBUF_DATA, 1, 0);
     if (!ring || nc_gpuhash_ring_debug_timeline(ring, 1, 0, NULL) != NC_OK) return 1;
     uint32_t *outs = malloc(maxk * sizeof(uint32_t));
-    enum { NMAX = 200000, NV = 9 };
+    enum { NMAX = 200000, NV = 10 };
     double *v[NV];
     for (int i = 0; i < NV; i++) v[i] = malloc(NMAX * sizeof(double));
     if (!outs) return 1;
@@ -113,6 +113,7 @@ static int ring_timeline(double seconds, struct mbuf *mb, uint32_t nmb, uint32_t
             v[6][n] = released > stored ? (double)(released - stored) * 0.01 : 0.0;
             v[7][n] = v[1][n] - v[0][n] - v[5][n] - v[6][n];
             v[8][n] = (double)tl[6]; /* the shader clock over the hash phase, MHz */
+            v[9][n] = tl[7] > tl[1] ? (double)(tl[7] - tl[1]) * 0.01 : 0.0; /* wave 0's own keys */
             n++;
         }
     }
@@ -124,8 +125,8 @@ static int ring_timeline(double seconds, struct mbuf *mb, uint32_t nmb, uint32_t
     printf("{\"point\": \"ring_timeline\", \"staging\": \"%s\", \"depth\": 1, \"threads\": %d, \"batches\": %d, \"median_us\": "
            "{\"host_submit_call\": %.2f, \"submit_to_done\": %.2f, \"dev_fetch\": %.2f, \"dev_hash\": %.2f, "
            "\"dev_store_ack\": %.2f, \"dev_found_to_stored\": %.2f, \"dev_release\": %.2f, "
-           "\"rest_detect_done_reap\": %.2f}, \"hash_clock_mhz_median\": %.0f, \"mismatches\": %" PRIu64 "}\n",
-           nc_gpuhash_ring_debug_staging(ring) == 1 ? "device" : "host", NC_GPUHASH_RING_DEFAULT_THREADS, n, med[0], med[1], med[2], med[3], med[4], med[5], med[6], med[7], med[8], bad);
+           "\"rest_detect_done_reap\": %.2f}, \"hash_clock_mhz_median\": %.0f, \"wave0_own_hash_us\": %.2f, \"mismatches\": %" PRIu64 "}\n",
+           nc_gpuhash_ring_debug_staging(ring) == 1 ? "device" : "host", NC_GPUHASH_RING_DEFAULT_THREADS, n, med[0], med[1], med[2], med[3], med[4], med[5], med[6], med[7], med[8], med[9], bad);
     nc_gpuhash_ring_destroy(ring);
     return bad ? 2 : 0;
 }

@@ -28,6 +28,9 @@ RUNS = [
                    "AVX2 stores and glibc memcpy, alternated twice on one box"),
     ("r06zo_deep", "DROPPED: the worker's byte readers two steps ahead (QStream kDeep, deep1) against one (deep0), "
                    "alternated twice on one box: the hash phase stays 1.88 us"),
+    ("r06zq_spread", "DROPPED: a batch's keys spread over all sixteen waves (x1) against the first ten (x0), "
+                     "alternated twice on one box: hash 2.32-2.36 us against 1.92; the timeline also reports the "
+                     "shader clock over the hash phase and wave 0's own share"),
 ]
 
 

@@ -352,6 +352,8 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
         case NC_GPUHASH_MURMUR: serve<NC_GPUHASH_MURMUR, T>(src, loff, nk, crc32t, so_out, wt); break;
         default: serve<NC_GPUHASH_JENKINS, T>(src, loff, nk, crc32t, so_out, wt); break;
         }
+        uint64_t t_own = 0; /* thread 0: its own wave's keys hashed (before waiting for the others) */
+        if (tl != nullptr && t == 0u) t_own = ticks();
         if (wt) { /* the hashes, in LDS, out 16 bytes a lane (up to 3 words past nk: within the slot's ostride) */
             __syncthreads();
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(so_out, 0, 4u * ostride, 0x00020000);
@@ -373,6 +375,7 @@ __global__ __launch_bounds__(T) void nc_ring_worker(RingCtl *ctl, RingDev *dv, c
                 __hip_atomic_store(&tl[8 * s + 1], (uint64_t)(t_staged), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&tl[8 * s + 2], (uint64_t)(t_issued), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&tl[8 * s + 3], (uint64_t)(ticks()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&tl[8 * s + 7], t_own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 /* [6]: the shader clock over the hash phase, MHz (cycles per 10 ns tick x 100) */
                 __hip_atomic_store(&tl[8 * s + 6], t_issued > t_staged ? (c_issued - c_staged) * 100u / (t_issued - t_staged) : 0u,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
